@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark (BASELINE.json metric) for the MI355X-native
+wavefront path tracer.
+
+Workload (BASELINE.json configs[1], "config 2"): scenes/portal_cornell.pbrt --
+closed Cornell interior lit by an aaplane emitter behind one axis-aligned
+portal, PathIntegrator maxdepth 5, 1920x1080, Halton 256 spp, box filter,
+portal strategy "portal".  Synthetic scene (no downloads).
+
+A step = one full 1920x1080 x 256-spp frame per rank.  Ranks shard the
+camera-sample index space (rank r renders samples [256 r, 256 r + 256) of
+every pixel: weak scaling, independent units, no data-path collective); the
+film accumulators are summed once per step with an RCCL reduce to rank 0
+(the only collective, inside the timed region).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "pbrt-v3-light-portals_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "Msamples/sec + Mrays/sec, 1920x1080 path integrator @256spp, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default=os.path.join(REPO, "scenes", "portal_cornell.pbrt"))
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per rank (0 = scene)")
+    ap.add_argument("--res", default="", help="override WxH")
+    ap.add_argument("--strategy", default="", help="override portal strategy")
+    ap.add_argument("--batch-slots", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def scene_text(args) -> str:
+    import re
+    txt = open(args.scene).read()
+    if args.res:
+        w, h = (int(v) for v in args.res.lower().split("x"))
+        txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [%d]' % w, txt)
+        txt = re.sub(r'"integer yresolution" \[\d+\]', '"integer yresolution" [%d]' % h, txt)
+    if args.spp:
+        txt = re.sub(r'"integer pixelsamples" \[\d+\]', '"integer pixelsamples" [%d]' % args.spp, txt)
+    if args.strategy:
+        txt = re.sub(r'"string strategy" "\w+"', '"string strategy" "%s"' % args.strategy, txt)
+    return txt
+
+
+def cpu_baseline(scene_path: str, seconds: float) -> dict:
+    """Reference CPU path restated in C (oracle/, 'port'), timed on this host's
+    cores on a bounded sample: the first T 16x16 tiles of the same frame."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    import ptgpu
+    hs = ptgpu.HostScene(scene_path)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=2 * threads)
+    dt = time.perf_counter() - t0
+    rate = st["samples"] / dt
+    tiles = int(max(2 * threads, min(4000, rate * seconds / (256 * 256))))
+    t0 = time.perf_counter()
+    _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=tiles)
+    dt = time.perf_counter() - t0
+    return {"value": round(st["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"first {tiles} 16x16 tiles of the same frame at the scene's spp "
+                      f"({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
+            "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import ptgpu
+
+    tmpdir = os.environ.get("TMPDIR", "/tmp")
+    spath = os.path.join(tmpdir, f"bench_scene_{os.getpid()}.pbrt")
+    with open(spath, "w") as f:
+        f.write(scene_text(args))
+    hs = ptgpu.HostScene(spath)
+    sc = ptgpu.Scene(hs, device=local, batch_slots=args.batch_slots or None)
+    w, h = sc.film_size()
+    import re
+    spp = int(re.search(r'"integer pixelsamples" \[(\d+)\]', open(spath).read()).group(1))
+    accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream().cuda_stream
+    s_begin, s_end = rank * spp, (rank + 1) * spp
+
+    def step():
+        accum.zero_()
+        st = sc.render_range_device(0, 1, s_begin, s_end, accum.data_ptr(), stream)
+        if world > 1:
+            dist.reduce(accum, dst=0)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agg = {"samples": 0, "closest_rays": 0, "shadow_rays": 0, "node_visits": 0, "prim_tests": 0, "trace_ms": 0.0,
+           "trace_launches": 0}
+    for _ in range(args.steps):
+        st = step()
+        for k in agg:
+            agg[k] += st[k]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tot = torch.tensor([agg["samples"], agg["closest_rays"] + agg["shadow_rays"]], dtype=torch.float64,
+                           device=f"cuda:{local}")
+        dist.all_reduce(tot)
+        total_samples, total_rays = float(tot[0]), float(tot[1])
+    else:
+        total_samples, total_rays = float(agg["samples"]), float(agg["closest_rays"] + agg["shadow_rays"])
+
+    if rank == 0:
+        alg_bytes = 32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]
+        achieved = alg_bytes / (agg["trace_ms"] * 1e-3) / 1e9 if agg["trace_ms"] > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": round(total_samples / dt / 1e6, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)",
+            "config": {"workload": f"portal Cornell (config 2) {w}x{h} @{spp}spp/rank, path maxdepth 5, "
+                                   f"sample-range sharded", "resolution": [w, h], "spp_per_rank": spp,
+                       "parallelism": f"sample-range x{world}"},
+            "mrays_per_s": round(total_rays / dt / 1e6, 2),
+            "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "k_trace", "algorithmic_bytes_per_launch": round(
+                             alg_bytes / max(1, agg["trace_launches"]), 1),
+                         "avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(spath, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    try:
+        os.remove(spath)
+    except OSError:
+        pass
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,301 @@
+/*
+ * pt.h -- C ABI of the MI355X-native wavefront path tracer.
+ *
+ * This is the drop-in boundary for the reference's SamplerIntegrator plugin
+ * surface.  A pbrt-v3 build binds these symbols from a `GpuPathIntegrator`
+ * registered in RenderOptions::MakeIntegrator:
+ *
+ *   reference interface                                     replaced by
+ *   ------------------------------------------------------  -----------------------------
+ *   Integrator::Render(const Scene&)                        pt_render / pt_render_tiles
+ *     src/core/integrator.h:53-58, integrator.cpp:526-637
+ *   PathIntegrator::Li(...)  src/integrators/path.cpp:64-189  (device wavefront, no host call)
+ *   CreatePathIntegrator(ParamSet, Sampler, Camera)         pt_integrator_desc
+ *     src/integrators/path.cpp:191-214
+ *   CreateHaltonSampler  src/samplers/halton.cpp:133-139    pt_sampler_desc
+ *   CreatePerspectiveCamera  src/cameras/perspective.cpp    pt_camera_desc
+ *   CreateFilm / CreateBoxFilter / CreateGaussianFilter     pt_film_desc
+ *     src/core/film.cpp:213-252, src/filters/{box,gaussian}.cpp
+ *   Scene{aggregate, lights}  src/core/scene.h:50-80         pt_scene_desc + pt_scene_create
+ *   CreateBVHAccelerator  src/accelerators/bvh.cpp:740-760   built inside pt_scene_create
+ *   MakeShapes "trianglemesh"/"aaplane"  src/core/api.cpp:432-546   pt_triangle / pt_aaplane
+ *   MakeAreaLight "diffuse"/"portal"  src/core/api.cpp:768-786      pt_light
+ *   CreateAAPortal  src/lights/portal_arealight.cpp:245-300          pt_light + pt_portal
+ *   pbrtParseFile  src/core/parser.cpp:1094                 pt_load_pbrt (host scene loader)
+ *   Film::WriteImage  src/core/film.cpp:169-211              pt_write_pfm
+ *
+ * Conventions: plain pointers + sizes, no C++ types, no exceptions across the
+ * boundary.  Every call returns pt_status; pt_last_error() gives a message.
+ * All host arrays passed in are copied; the caller keeps ownership.  All
+ * calls for one device come from one host thread.
+ */
+#ifndef PT_H
+#define PT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+typedef enum pt_status {
+    PT_OK = 0,
+    PT_ERR_INVALID_ARG = 1,
+    PT_ERR_PARSE = 2,
+    PT_ERR_UNSUPPORTED = 3,
+    PT_ERR_DEVICE = 4,
+    PT_ERR_OOM = 5,
+    PT_ERR_STATE = 6,
+    PT_ERR_IO = 7
+} pt_status;
+
+/* ---- scene description (world space, the reference's post-parse Scene) ---- */
+
+enum pt_prim_kind { PT_PRIM_TRIANGLE = 0, PT_PRIM_AAPLANE = 1 };
+
+enum pt_material_kind {
+    PT_MAT_NONE = 0,   /* "" / "none": null BSDF, path passes through   */
+    PT_MAT_MATTE = 1   /* MatteMaterial  src/materials/matte.cpp:45-62 */
+};
+
+enum pt_light_kind {
+    PT_LIGHT_DIFFUSE_AREA = 0, /* DiffuseAreaLight on one triangle   src/lights/diffuse.cpp */
+    PT_LIGHT_PORTAL_AREA = 1   /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
+};
+
+enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:12 */
+    PT_PORTAL_LIGHT = 0,       /* "light"      SampleUniformLight */
+    PT_PORTAL_UNIFORM = 1,     /* "portal"     SampleUniformPortal */
+    PT_PORTAL_PROJECTION = 2   /* "projection" SampleProjection */
+};
+
+enum pt_filter_kind { PT_FILTER_BOX = 0, PT_FILTER_GAUSSIAN = 1 };
+
+enum pt_light_sample_strategy { PT_LIGHTS_UNIFORM = 0, PT_LIGHTS_POWER = 1 };
+
+/* Transform (src/core/transform.h): m and its stored inverse mInv, row-major. */
+typedef struct pt_transform {
+    float m[16];
+    float minv[16];
+} pt_transform;
+
+/* Flags on a triangle (bit set). */
+#define PT_TRI_REVERSE_ORIENTATION 1u  /* Shape::reverseOrientation */
+#define PT_TRI_SWAPS_HANDEDNESS 2u     /* Shape::transformSwapsHandedness */
+#define PT_TRI_HAS_N 4u                /* TriangleMesh::n present */
+#define PT_TRI_HAS_UV 8u               /* TriangleMesh::uv present */
+#define PT_TRI_HAS_S 16u               /* TriangleMesh::s present */
+
+/* One Triangle shape (src/shapes/triangle.h); vertices are already in world
+ * space (TriangleMesh ctor, triangle.cpp:75). */
+typedef struct pt_triangle {
+    int32_t v[3];        /* indices into pt_scene_desc vertex arrays */
+    int32_t material;    /* index into materials */
+    int32_t area_light;  /* index into lights, or -1 */
+    uint32_t flags;      /* PT_TRI_* */
+} pt_triangle;
+
+/* AAPlaneShape (src/shapes/plane.h:12-70). lo/hi are object space. */
+typedef struct pt_aaplane {
+    float lo[3];
+    float hi[3];
+    int32_t axis;
+    int32_t material;
+    int32_t area_light;
+    uint32_t flags;                /* PT_TRI_REVERSE_ORIENTATION | PT_TRI_SWAPS_HANDEDNESS */
+    pt_transform object_to_world;  /* m = ObjectToWorld, minv = WorldToObject */
+} pt_aaplane;
+
+/* Primitive in scene order (RenderOptions::primitives, api.cpp:1431-1433). */
+typedef struct pt_prim {
+    int32_t kind;   /* pt_prim_kind */
+    int32_t index;  /* into triangles or planes */
+} pt_prim;
+
+typedef struct pt_material {
+    int32_t kind;   /* pt_material_kind */
+    float kd[3];    /* constant Kd (already Clamp()ed is NOT assumed) */
+    float sigma;    /* OrenNayar sigma in degrees; only 0 supported */
+} pt_material;
+
+/* AAPortal (src/portals/aaportal.h) as parsed from portalData. */
+typedef struct pt_portal {
+    float lo[3];
+    float hi[3];
+    int32_t axis;
+    int32_t facing_fw;
+} pt_portal;
+
+typedef struct pt_light {
+    int32_t kind;         /* pt_light_kind */
+    float L[3];           /* Lemit = L * scale */
+    int32_t two_sided;
+    int32_t shape;        /* triangle index (diffuse) or plane index (portal) */
+    int32_t strategy;     /* pt_portal_strategy (portal lights) */
+    int32_t first_portal; /* into portals */
+    int32_t n_portals;
+} pt_light;
+
+typedef struct pt_camera_desc {
+    pt_transform camera_to_world;  /* RenderOptions::CameraToWorld */
+    float fov;
+    float screen_window[4];        /* xmin, xmax, ymin, ymax */
+    float lens_radius;
+    float focal_distance;
+    float shutter_open;
+    float shutter_close;
+} pt_camera_desc;
+
+typedef struct pt_film_desc {
+    int32_t xres, yres;
+    float crop[4];                 /* xmin, xmax, ymin, ymax in [0,1] */
+    int32_t filter;                /* pt_filter_kind */
+    float filter_radius[2];
+    float gaussian_alpha;
+    float scale;
+    float max_sample_luminance;
+    float diagonal;
+} pt_film_desc;
+
+typedef struct pt_sampler_desc {
+    int32_t spp;
+    int32_t sample_pixel_center;
+} pt_sampler_desc;
+
+typedef struct pt_integrator_desc {
+    int32_t max_depth;
+    float rr_threshold;
+    int32_t light_strategy;        /* pt_light_sample_strategy */
+    int32_t has_pixel_bounds;
+    int32_t pixel_bounds[4];       /* x0, x1, y0, y1 as in the "pixelbounds" param */
+} pt_integrator_desc;
+
+typedef struct pt_scene_desc {
+    int32_t n_vertices;
+    const float* P;     /* 3*n_vertices, world space */
+    const float* N;     /* 3*n_vertices or NULL */
+    const float* S;     /* 3*n_vertices or NULL */
+    const float* UV;    /* 2*n_vertices or NULL */
+    int32_t n_triangles;
+    const pt_triangle* triangles;
+    int32_t n_planes;
+    const pt_aaplane* planes;
+    int32_t n_prims;
+    const pt_prim* prims;
+    int32_t n_materials;
+    const pt_material* materials;
+    int32_t n_lights;
+    const pt_light* lights;
+    int32_t n_portals;
+    const pt_portal* portals;
+    int32_t bvh_max_prims;          /* "maxnodeprims", default 4 */
+    pt_camera_desc camera;
+    pt_film_desc film;
+    pt_sampler_desc sampler;
+    pt_integrator_desc integrator;
+} pt_scene_desc;
+
+/* ---- statistics (reference counters, src/core/scene.cpp:40-42 etc.) ---- */
+typedef struct pt_stats {
+    uint64_t camera_rays;      /* "Integrator/Camera rays traced" */
+    uint64_t closest_rays;     /* "Regular ray intersection tests" */
+    uint64_t shadow_rays;      /* "Shadow ray intersection tests" */
+    uint64_t node_visits;      /* BVH nodes whose bounds were tested */
+    uint64_t prim_tests;       /* leaf primitive intersection tests */
+    uint64_t samples;          /* camera samples rendered */
+    double render_ms;          /* device wall time of the render (events) */
+    double trace_ms;           /* summed duration of the trace kernel */
+    uint64_t trace_launches;
+} pt_stats;
+
+/* ---- host scene loader (.pbrt subset) ---- */
+typedef struct pt_host_scene pt_host_scene;
+
+pt_status pt_load_pbrt(const char* path, pt_host_scene** out);
+const pt_scene_desc* pt_host_scene_desc(const pt_host_scene* hs);
+void pt_host_scene_free(pt_host_scene* hs);
+
+/* ---- device scene + render ---- */
+typedef struct pt_scene pt_scene;
+
+int pt_abi_version(void);
+const char* pt_last_error(void);
+
+/* Select the HIP device for this host thread. */
+pt_status pt_init(int device);
+
+/* Build the SAH BVH on the host (BVHAccel, bvh.cpp:236-402) and upload the
+ * flattened scene to device memory. */
+pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out);
+void pt_scene_destroy(pt_scene* scene);
+
+/* Read back the flattened BVH (32-byte LinearBVHNode records, bvh.cpp:95-104)
+ * and the primitive order, for parity tests.  Pass NULL to query counts. */
+pt_status pt_scene_bvh(const pt_scene* scene, int32_t* n_nodes, void* nodes32,
+                       int32_t* n_prims, int32_t* prim_order);
+
+/* Host-only BVH build (no device needed): same nodes as pt_scene_bvh. */
+pt_status pt_build_bvh_host(const pt_scene_desc* desc, int32_t* n_nodes, void* nodes32,
+                            int32_t* prim_order, int32_t cap);
+
+/* Render the whole sample-bound region serially on this device and write the
+ * final RGB image (croppedPixelBounds, 3 floats per pixel, WriteImage
+ * semantics) to rgb_out.  stats may be NULL. */
+pt_status pt_render(pt_scene* scene, float* rgb_out, pt_stats* stats);
+
+/* Multi-GPU building block: render the 16x16 image tiles t with
+ * t % tile_stride == tile_offset into a device-resident accumulation buffer
+ * (4 floats per cropped pixel: RGB contribution sum + filter weight sum,
+ * zeroed by the caller), on `stream` (hipStream_t, may be NULL).  Returns
+ * when the work is enqueued; the caller synchronises. */
+pt_status pt_render_tiles(pt_scene* scene, int tile_offset, int tile_stride,
+                          float* d_accum, void* stream, pt_stats* stats);
+
+/* Same as pt_render_tiles for camera-sample indices [sample_begin,
+ * sample_end) of every pixel (the Halton sequence continues past the scene's
+ * spp), so N ranks can each render a disjoint sample range of one frame. */
+pt_status pt_render_range(pt_scene* scene, int tile_offset, int tile_stride,
+                          int sample_begin, int sample_end, float* d_accum,
+                          void* stream, pt_stats* stats);
+
+/* Resolve an accumulation buffer (host memory, 4 floats per pixel) into the
+ * final RGB image exactly as Film::MergeFilmTile + Film::WriteImage do. */
+pt_status pt_resolve_film(const pt_scene* scene, const float* accum, float* rgb_out);
+
+/* Same as pt_render_tiles but synchronous, into a host buffer (4 floats per
+ * cropped pixel, zero-initialised by the call). */
+pt_status pt_render_accum(pt_scene* scene, int tile_offset, int tile_stride,
+                          float* accum_out, pt_stats* stats);
+
+/* Number of in-flight paths per wavefront batch (default 8M).  Memory for
+ * path state is ~230 bytes per slot. */
+pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
+
+/* Number of cropped pixels (rgb_out holds 3x this many floats). */
+pt_status pt_film_size(const pt_scene* scene, int32_t* width, int32_t* height);
+
+/* Film::WriteImage to a PFM file (imageio.cpp WritePFM). */
+pt_status pt_write_pfm(const char* path, const float* rgb, int32_t width, int32_t height);
+
+/* ---- test hooks (used by the parity tests; not part of the render path) ---- */
+/* The shared host/device sinf/cosf port used by ConcentricSampleDisk,
+ * evaluated on the host (compare with the platform libm). */
+pt_status pt_debug_libm_trig(int n, const float* x, float* sin_out, float* cos_out);
+/* HaltonSampler::SampleDimension(idx[i], dims[i]) on the device. */
+pt_status pt_debug_halton(pt_scene* scene, int n, const uint32_t* idx, const int32_t* dims, float* out);
+/* HaltonSampler per-pixel offsets for (x, y) pairs. */
+pt_status pt_debug_pixel_offsets(pt_scene* scene, int n, const int32_t* pixxy, uint32_t* out);
+/* Camera rays (o, d) for film positions (pLens = (0.5, 0.5)). */
+pt_status pt_debug_camera_rays(pt_scene* scene, int n, const float* film_xy, float* out6);
+/* BVH traversal for rays (o, d, tMax): closest primitive index in BVH order
+ * (any = 0) or occlusion flag (any = 1); -1 for a miss. */
+pt_status pt_debug_trace(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PT_H */

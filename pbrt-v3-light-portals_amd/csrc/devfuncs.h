@@ -1,0 +1,415 @@
+// devfuncs.h -- device functions of the hot path (gfx950).  Each restates a
+// reference function (file:line cited) with the same float operation order.
+#pragma once
+
+#include "device.h"
+
+namespace pt {
+
+// ----------------------------------------------------------------------------
+// Halton sampler: HaltonSampler::SampleDimension (samplers/halton.cpp:118-127)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float radical_inverse_base3(uint32_t a) {  // lowdiscrepancy.cpp:389-403
+    const float invBase = 1.0f / 3.0f;
+    uint64_t rev = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint32_t next = a / 3u;
+        uint32_t digit = a - next * 3u;
+        rev = rev * 3u + digit;
+        invBaseN *= invBase;
+        a = next;
+    }
+    return smin((float)rev * invBaseN, kOneMinusEps);
+}
+
+__device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, int dim, uint32_t a) {  // :405-424
+    const DivMagic dm = sc.divs[dim];
+    const uint16_t* perm = sc.perm + sc.prime_sums[dim];
+    uint64_t rev = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint32_t next = fast_div(a, dm);
+        uint32_t digit = a - next * dm.base;
+        rev = rev * dm.base + perm[digit];
+        invBaseN *= dm.inv_base;
+        a = next;
+    }
+    return smin(invBaseN * ((float)rev + sc.perm_c0[dim]), kOneMinusEps);
+}
+
+// dim must be < sc.max_dim (checked by the caller).
+__device__ __forceinline__ float halton_dim(const DevScene& sc, uint32_t idx, int dim) {
+    if (sc.center && dim < 2) return 0.5f;
+    if (dim == 0) return (float)reverse_bits32(idx >> sc.hal_exp0) * 0x1p-32f;  // RadicalInverse(0, .)
+    if (dim == 1) return radical_inverse_base3(fast_div(idx, sc.div_scale1));
+    return scrambled_radical_inverse(sc, dim, idx);
+}
+
+// Per-pixel Halton offset (halton.cpp:96-113); values stay far below 2^32.
+__device__ __forceinline__ uint32_t halton_pixel_offset(const DevScene& sc, int px, int py, int exp1,
+                                                        uint32_t scale0, uint32_t mi0, uint32_t mi1) {
+    uint32_t stride = sc.hal_stride;
+    if (stride <= 1) return 0;
+    int pmx = px % 128; if (pmx < 0) pmx += 128;
+    int pmy = py % 128; if (pmy < 0) pmy += 128;
+    uint64_t off = 0;
+    {   // InverseRadicalInverse<2>(pm.x, exp0)
+        uint64_t inv = (uint64_t)pmx, index = 0;
+        for (int i = 0; i < sc.hal_exp0; ++i) { uint64_t d = inv % 2u; inv /= 2u; index = index * 2u + d; }
+        off += index * (uint64_t)(stride / scale0) * (uint64_t)mi0;
+    }
+    {   // InverseRadicalInverse<3>(pm.y, exp1)
+        uint64_t inv = (uint64_t)pmy, index = 0;
+        for (int i = 0; i < exp1; ++i) { uint64_t d = inv % 3u; inv /= 3u; index = index * 3u + d; }
+        off += index * (uint64_t)(stride / sc.hal_scale1) * (uint64_t)mi1;
+    }
+    return (uint32_t)(off % stride);
+}
+
+// ----------------------------------------------------------------------------
+// Triangle::Intersect / IntersectP ray-triangle test (triangle.cpp:189-292)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ bool tri_test(V3 p0, V3 p1, V3 p2, const Ray& ray, float* tHit, float* b0o,
+                                         float* b1o, float* b2o) {
+    V3 p0t = p0 - ray.o, p1t = p1 - ray.o, p2t = p2 - ray.o;
+    int kz = maxdim(vabs(ray.d));
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    V3 d = permute(ray.d, kx, ky, kz);
+    p0t = permute(p0t, kx, ky, kz);
+    p1t = permute(p1t, kx, ky, kz);
+    p2t = permute(p2t, kx, ky, kz);
+    float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1.f / d.z;
+    p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
+    float e0 = p1t.x * p2t.y - p1t.y * p2t.x;
+    float e1 = p2t.x * p0t.y - p2t.y * p0t.x;
+    float e2 = p0t.x * p1t.y - p0t.y * p1t.x;
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double p2txp1ty = (double)p2t.x * (double)p1t.y;
+        double p2typ1tx = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(p2typ1tx - p2txp1ty);
+        double p0txp2ty = (double)p0t.x * (double)p2t.y;
+        double p0typ2tx = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(p0typ2tx - p0txp2ty);
+        double p1txp0ty = (double)p1t.x * (double)p0t.y;
+        double p1typ0tx = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(p1typ0tx - p1txp0ty);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz; p1t.z *= Sz; p2t.z *= Sz;
+    float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < ray.tmax * det)) return false;
+    else if (det > 0 && (tScaled <= 0 || tScaled > ray.tmax * det)) return false;
+    float invDet = 1 / det;
+    float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    float t = tScaled * invDet;
+    float maxZt = maxcomp(vabs(v3(p0t.z, p1t.z, p2t.z)));
+    float deltaZ = gammaf(3) * maxZt;
+    float maxXt = maxcomp(vabs(v3(p0t.x, p1t.x, p2t.x)));
+    float maxYt = maxcomp(vabs(v3(p0t.y, p1t.y, p2t.y)));
+    float deltaX = gammaf(5) * (maxXt + maxZt);
+    float deltaY = gammaf(5) * (maxYt + maxZt);
+    float deltaE = 2 * (gammaf(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    float maxE = maxcomp(vabs(v3(e0, e1, e2)));
+    float deltaT = 3 * (gammaf(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * fabsf(invDet);
+    if (t <= deltaT) return false;
+    *tHit = t;
+    *b0o = b0; *b1o = b1; *b2o = b2;
+    return true;
+}
+
+// ----------------------------------------------------------------------------
+// AAPlaneShape::Intersect (plane.cpp:15-55) -- test part
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ bool plane_test(const DevPlane& pl, const Ray& ray, float* tHit, V3* pHitObj) {
+    Ray rT = xf_ray_keep_tmax(pl.w2o, ray);
+    float t = (pl.lo[pl.ax] - rT.o[pl.ax]) / rT.d[pl.ax];
+    V3 pHit = rT.o + t * rT.d;
+    if (pHit[pl.ax0] > pl.lo[pl.ax0] && pHit[pl.ax0] < pl.hi[pl.ax0] && pHit[pl.ax1] > pl.lo[pl.ax1] &&
+        pHit[pl.ax1] < pl.hi[pl.ax1] && t < rT.tmax) {
+        *tHit = t;
+        *pHitObj = pHit;
+        return true;
+    }
+    return false;
+}
+
+struct SurfHit {
+    V3 p, perr, n, wo;
+    V3 sn, sdpdu;
+    int prim;  // BVH-order primitive index
+};
+
+__device__ __forceinline__ V3 vload3(const float* a, int i) { return v3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }
+
+// Full Triangle::Intersect for the winning primitive: SurfaceInteraction
+// (triangle.cpp:297-420, interaction.cpp:44-89).  Returns false when the
+// reference would reject (it never does for the primitive that won in the
+// traversal, which already applied the same tests).
+__device__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si) {
+    const pt_triangle tr = sc.tris[ti];
+    V3 p0 = vload3(sc.P, tr.v[0]), p1 = vload3(sc.P, tr.v[1]), p2 = vload3(sc.P, tr.v[2]);
+    Ray r2 = ray;
+    r2.tmax = kInf;
+    float t, b0, b1, b2;
+    if (!tri_test(p0, p1, p2, r2, &t, &b0, &b1, &b2)) return false;
+    float uv[3][2];
+    bool hasUV = (tr.flags & PT_TRI_HAS_UV) && sc.UV;
+    if (hasUV) {
+        for (int i = 0; i < 3; ++i) { uv[i][0] = sc.UV[2 * tr.v[i]]; uv[i][1] = sc.UV[2 * tr.v[i] + 1]; }
+    } else {
+        uv[0][0] = 0; uv[0][1] = 0; uv[1][0] = 1; uv[1][1] = 0; uv[2][0] = 1; uv[2][1] = 1;
+    }
+    float duv02[2] = {uv[0][0] - uv[2][0], uv[0][1] - uv[2][1]};
+    float duv12[2] = {uv[1][0] - uv[2][0], uv[1][1] - uv[2][1]};
+    V3 dp02 = p0 - p2, dp12 = p1 - p2;
+    float determinant = duv02[0] * duv12[1] - duv02[1] * duv12[0];
+    bool degenerateUV = fabs((double)determinant) < 1e-8;
+    V3 dpdu = v3(0, 0, 0), dpdv = v3(0, 0, 0);
+    if (!degenerateUV) {
+        float invdet = 1 / determinant;
+        dpdu = (duv12[1] * dp02 - duv02[1] * dp12) * invdet;
+        dpdv = (-duv12[0] * dp02 + duv02[0] * dp12) * invdet;
+    }
+    if (degenerateUV || len2(cross(dpdu, dpdv)) == 0) {
+        V3 ng = cross(p2 - p0, p1 - p0);
+        if (len2(ng) == 0) return false;
+        coordinate_system(normalize(ng), &dpdu, &dpdv);
+    }
+    float xs = fabsf(b0 * p0.x) + fabsf(b1 * p1.x) + fabsf(b2 * p2.x);
+    float ys = fabsf(b0 * p0.y) + fabsf(b1 * p1.y) + fabsf(b2 * p2.y);
+    float zs = fabsf(b0 * p0.z) + fabsf(b1 * p1.z) + fabsf(b2 * p2.z);
+    si->perr = gammaf(7) * v3(xs, ys, zs);
+    si->p = (b0 * p0 + b1 * p1) + b2 * p2;
+    si->wo = normalize(-ray.d);
+    V3 n = normalize(cross(dp02, dp12));
+    bool ro = (tr.flags & PT_TRI_REVERSE_ORIENTATION) != 0;
+    bool sh = (tr.flags & PT_TRI_SWAPS_HANDEDNESS) != 0;
+    if (ro ^ sh) n = -n;
+    si->n = n;
+    si->sn = n;
+    si->sdpdu = dpdu;
+    bool hasN = (tr.flags & PT_TRI_HAS_N) && sc.N;
+    bool hasS = (tr.flags & PT_TRI_HAS_S) && sc.S;
+    if (hasN || hasS) {
+        V3 ns;
+        if (hasN) {
+            ns = (b0 * vload3(sc.N, tr.v[0]) + b1 * vload3(sc.N, tr.v[1])) + b2 * vload3(sc.N, tr.v[2]);
+            ns = (len2(ns) > 0) ? normalize(ns) : si->n;
+        } else
+            ns = si->n;
+        V3 ss;
+        if (hasS) {
+            ss = (b0 * vload3(sc.S, tr.v[0]) + b1 * vload3(sc.S, tr.v[1])) + b2 * vload3(sc.S, tr.v[2]);
+            ss = (len2(ss) > 0) ? normalize(ss) : normalize(dpdu);
+        } else
+            ss = normalize(dpdu);
+        V3 ts = cross(ss, ns);
+        if (len2(ts) > 0.f) { ts = normalize(ts); ss = cross(ts, ns); }
+        else coordinate_system(ns, &ss, &ts);
+        if (ro) ts = -ts;
+        si->sn = normalize(cross(ss, ts));  // SetShadingGeometry(..., true)
+        si->n = faceforward(si->n, si->sn);
+        si->sdpdu = ss;
+    }
+    return true;
+}
+
+// Full AAPlaneShape::Intersect SurfaceInteraction, transformed to world space
+// (plane.cpp:35-50, transform.cpp:262-297).
+__device__ bool plane_surface(const DevPlane& pl, const Ray& ray, SurfHit* si) {
+    Ray r2 = ray;
+    r2.tmax = kInf;
+    float t;
+    V3 pHit;
+    if (!plane_test(pl, r2, &t, &pHit)) return false;
+    V3 dpdu = v3(-1, 0, 0), dpdv = v3(0, 1, 0);
+    V3 n = normalize(cross(dpdu, dpdv));
+    V3 sn = n;
+    if (pl.ro_xor_sh) { n = n * -1.f; sn = sn * -1.f; }
+    V3 wo = normalize(-ray.d);
+    si->p = xf_point_err_in(pl.o2w, pHit, v3(0.01f, 0.01f, 0.01f), &si->perr);
+    si->n = normalize(xf_normal(pl.w2o, n));
+    si->wo = normalize(xf_vector(pl.o2w, wo));
+    si->sn = normalize(xf_normal(pl.w2o, sn));
+    si->sdpdu = xf_vector(pl.o2w, dpdu);
+    si->sn = faceforward(si->sn, si->n);
+    return true;
+}
+
+__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
+    float4 r0 = sc.prims[3 * prim];
+    float4 r1 = sc.prims[3 * prim + 1];
+    uint32_t flags = __float_as_uint(r0.w);
+    int idx = __float_as_int(r1.w);
+    bool ok = (flags & kPrimPlane) ? plane_surface(sc.planes[idx], ray, si) : tri_surface(sc, idx, ray, si);
+    si->prim = prim;
+    return ok;
+}
+
+__device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
+    float4 r0 = sc.prims[3 * prim];
+    float4 r1 = sc.prims[3 * prim + 1];
+    uint32_t flags = __float_as_uint(r0.w);
+    int idx = __float_as_int(r1.w);
+    if (flags & kPrimPlane) {
+        *material = sc.planes[idx].material;
+        *light = sc.planes[idx].area_light;
+    } else {
+        const pt_triangle& t = sc.tris[idx];
+        *material = t.material;
+        *light = t.area_light;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// BSDF: MatteMaterial (matte.cpp:45-62) -> BSDF{LambertianReflection}
+// (reflection.h:167-213, reflection.cpp:211-213, 416-427, 713-829)
+// ----------------------------------------------------------------------------
+struct Bsdf {
+    int nbxdf;
+    S3 R;
+    V3 ns, ng, ss, ts;
+};
+
+__device__ __forceinline__ void make_bsdf(const pt_material& m, const SurfHit& si, Bsdf* b) {
+    b->ns = si.sn;
+    b->ng = si.n;
+    b->ss = normalize(si.sdpdu);
+    b->ts = cross(b->ns, b->ss);
+    S3 r = s3(m.kd[0], m.kd[1], m.kd[2]);
+    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : r.c[i];  // Spectrum::Clamp()
+    b->nbxdf = is_black(r) ? 0 : 1;
+    b->R = r;
+}
+__device__ __forceinline__ V3 w2l(const Bsdf& b, V3 v) { return v3(dot(v, b.ss), dot(v, b.ts), dot(v, b.ns)); }
+__device__ __forceinline__ V3 l2w(const Bsdf& b, V3 v) {
+    return v3(b.ss.x * v.x + b.ts.x * v.y + b.ns.x * v.z, b.ss.y * v.x + b.ts.y * v.y + b.ns.y * v.z,
+              b.ss.z * v.x + b.ts.z * v.y + b.ns.z * v.z);
+}
+__device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW) {
+    V3 wo = w2l(b, woW);
+    if (wo.z == 0) return s3(0.f);
+    bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    S3 f = s3(0.f);
+    if (b.nbxdf && reflect) f = f + b.R * kInvPi;
+    return f;
+}
+__device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW) {
+    if (b.nbxdf == 0) return 0.f;
+    V3 wo = w2l(b, woW), wi = w2l(b, wiW);
+    if (wo.z == 0) return 0.f;
+    float pdf = 0.f;
+    pdf += (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    return pdf / 1;
+}
+// BSDF::Sample_f; returns false where the reference leaves *pdf unwritten
+// (wo.z == 0) -- f is black in that case.
+__device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf) {
+    if (b.nbxdf == 0) { *pdf = 0; return s3(0.f); }
+    int comp = (int)floorf(u0 * 1);
+    comp = (0 < comp) ? 0 : comp;  // std::min(comp, matchingComps - 1)
+    float ur0 = smin(u0 * 1 - comp, kOneMinusEps);
+    V3 wo = w2l(b, woW);
+    if (wo.z == 0) return s3(0.f);
+    V3 wi = cosine_sample_hemisphere(ur0, u1);
+    if (wo.z < 0) wi.z *= -1;
+    *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    if (*pdf == 0) return s3(0.f);
+    *wiW = l2w(b, wi);
+    bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
+    S3 f = s3(0.f);
+    if (reflect) f = f + b.R * kInvPi;
+    return f;
+}
+
+// ----------------------------------------------------------------------------
+// Lights: DiffuseAreaLight (lights/diffuse.{h,cpp}), AAPlaneShape sampling
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ S3 area_L(const DevLight& l, V3 n, V3 w) {  // diffuse.h:58-60
+    return (l.two_sided || dot(n, w) > 0) ? l.L : s3(0.f);
+}
+
+__device__ __forceinline__ V3 plane_normal(const DevPlane& pl) {  // plane.cpp:74-83
+    V3 r = v3(0, 0, 0);
+    r.set(pl.ax, 1);
+    if (!pl.facing_fw) r = r * -1.f;
+    return r;
+}
+__device__ __forceinline__ bool plane_in_front(const DevPlane& pl, V3 p) {  // plane.cpp:109-115
+    return pl.facing_fw ? (p[pl.ax] > pl.lo[pl.ax]) : (p[pl.ax] < pl.lo[pl.ax]);
+}
+__device__ __forceinline__ void plane_sample(const DevPlane& pl, float u0, float u1, V3* p, V3* n, V3* perr,
+                                             float* pdf) {  // plane.cpp:57-72
+    V3 loW = xf_point(pl.o2w, pl.lo), hiW = xf_point(pl.o2w, pl.hi);
+    V3 q = v3(0, 0, 0);
+    q.set(pl.ax, loW[pl.ax]);
+    q.set(pl.ax0, loW[pl.ax0] + (hiW[pl.ax0] - loW[pl.ax0]) * u0);
+    q.set(pl.ax1, loW[pl.ax1] + (hiW[pl.ax1] - loW[pl.ax1]) * u1);
+    *p = q;
+    *n = plane_normal(pl);
+    *perr = v3(0.1f, 0.1f, 0.1f);
+    *pdf = 1 / pl.area;
+}
+__device__ __forceinline__ void tri_sample(const DevScene& sc, int ti, float u0, float u1, V3* p, V3* n, V3* perr,
+                                           float* pdf) {  // triangle.cpp:584-609
+    const pt_triangle tr = sc.tris[ti];
+    float su0 = sqrtf(u0);
+    float b0 = 1 - su0, b1 = u1 * su0;
+    V3 p0 = vload3(sc.P, tr.v[0]), p1 = vload3(sc.P, tr.v[1]), p2 = vload3(sc.P, tr.v[2]);
+    float b2 = 1 - b0 - b1;
+    *p = (b0 * p0 + b1 * p1) + b2 * p2;
+    *n = normalize(cross(p1 - p0, p2 - p0));
+    if ((tr.flags & PT_TRI_HAS_N) && sc.N) {
+        V3 ns = (b0 * vload3(sc.N, tr.v[0]) + b1 * vload3(sc.N, tr.v[1])) + b2 * vload3(sc.N, tr.v[2]);
+        *n = faceforward(*n, ns);
+    } else if (((tr.flags & PT_TRI_REVERSE_ORIENTATION) != 0) ^ ((tr.flags & PT_TRI_SWAPS_HANDEDNESS) != 0)) {
+        *n = *n * -1.f;
+    }
+    V3 pa = (vabs(b0 * p0) + vabs(b1 * p1)) + vabs(b2 * p2);
+    *perr = gammaf(6) * pa;
+    *pdf = 1 / sc.tri_area[ti];
+}
+
+// DiffuseAreaLight::Sample_Li + Shape::Sample(ref, u, pdf) (diffuse.cpp:69-84, shape.cpp:56-74)
+__device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, float u0,
+                                             float u1, V3* wi, float* pdf, V3* sp, V3* sn, V3* spe) {
+    V3 p, n, pe;
+    if (l.kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l.shape, u0, u1, &p, &n, &pe, pdf);
+    else plane_sample(sc.planes[l.shape], u0, u1, &p, &n, &pe, pdf);
+    V3 w = p - ref.p;
+    if (len2(w) == 0) *pdf = 0;
+    else {
+        w = normalize(w);
+        *pdf *= dist2(ref.p, p) / absdot(n, -w);
+        if (__builtin_isinf(*pdf)) *pdf = 0.f;
+    }
+    if (*pdf == 0 || len2(p - ref.p) == 0) { *pdf = 0; return s3(0.f); }
+    *wi = normalize(p - ref.p);
+    *sp = p; *sn = n; *spe = pe;
+    return area_L(l, n, -*wi);
+}
+
+// Shape::Pdf(ref, wi) for the light's shape (shape.cpp:76-91)
+__device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, V3 wi) {
+    Ray r{offset_ray_origin(ref.p, ref.perr, ref.n, wi), wi, kInf};
+    SurfHit isl;
+    bool ok;
+    if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
+        // Triangle::Intersect on this one triangle (tMax = Infinity).
+        ok = tri_surface(sc, l.shape, r, &isl);
+    } else {
+        ok = plane_surface(sc.planes[l.shape], r, &isl);
+    }
+    if (!ok) return 0;
+    float pdf = dist2(ref.p, isl.p) / (absdot(isl.n, -wi) * l.area);
+    if (__builtin_isinf(pdf)) pdf = 0.f;
+    return pdf;
+}
+
+}  // namespace pt

@@ -1,0 +1,139 @@
+// device.h -- device-resident scene and path-state layouts shared by the
+// wavefront kernels (kernels.hip) and the host driver (render.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/pt.h"
+#include "ptmath.h"
+
+namespace pt {
+
+// AAPlaneShape with everything the kernels need precomputed
+// (src/shapes/plane.h:15-32): object-space lo/hi, axes, facingFw =
+// !reverseOrientation, and the ObjectToWorld / WorldToObject matrices.
+struct DevPlane {
+    V3 lo, hi;
+    int ax, ax0, ax1;
+    int facing_fw;
+    int ro_xor_sh;
+    int material;
+    int area_light;
+    float area;
+    M4 o2w, w2o;
+};
+
+struct DevLight {
+    int kind;
+    S3 L;
+    int two_sided;
+    int shape;
+    int strategy;
+    int first_portal;
+    int n_portals;
+    float area;
+};
+
+// Prim record flags (word 0 .w of the 48-byte record)
+constexpr uint32_t kPrimPlane = 1u;       // AAPlaneShape (else Triangle)
+constexpr uint32_t kPrimDegenerate = 2u;  // Triangle::Intersect always rejects (triangle.cpp:309-315)
+
+struct DevScene {
+    // BVH: 2 x float4 per LinearBVHNode; 3 x float4 per primitive in BVH order
+    const float4* nodes;
+    const float4* prims;
+    int n_nodes;
+    int n_prims;
+    const pt_triangle* tris;
+    const float* P;
+    const float* N;
+    const float* S;
+    const float* UV;
+    const DevPlane* planes;
+    const DevPlane* portal_planes;
+    const pt_material* mats;
+    const DevLight* lights;
+    int n_lights;
+    const float* ldist_func;
+    const float* ldist_cdf;
+    float ldist_int;
+    const float* tri_area;
+    // Halton sampler (samplers/halton.cpp)
+    const uint16_t* perm;
+    const int* prime_sums;
+    const DivMagic* divs;   // per dimension: prime base, magic, shift, 1/base
+    const float* perm_c0;   // per dimension: invBase * perm[0] / (1 - invBase)
+    int max_dim;
+    int hal_exp0;
+    uint32_t hal_scale1;
+    DivMagic div_scale1;
+    uint32_t hal_stride;
+    int center;
+    // camera (cameras/perspective.cpp)
+    M4 r2c;
+    M4 c2w;
+    float lens_radius, focal_distance;
+    // integrator (integrators/path.cpp)
+    int max_depth;
+    float rr_threshold;
+};
+
+// Per-path SoA state for one batch of nslots camera samples.
+struct DevPaths {
+    int n;
+    uint32_t* hidx;     // Halton index of the sample
+    float2* pfilm;      // CameraSample::pFilm
+    float* L;           // 3n
+    float* beta;        // 3n
+    float* eta;         // n
+    uint32_t* st;       // n: packed state, see kSt* below
+    float* ray;         // 6n continuation ray o,d
+    int* hit;           // n
+    float* rayA;        // 7n NEE ray A o,d,tMax
+    int* hitA;          // n
+    float* rayB;        // 6n NEE ray B o,d
+    int* hitB;          // n
+    float* nee;         // kNee * n payload
+};
+
+// st bits
+constexpr uint32_t kStDimMask = 0xffffu;
+constexpr uint32_t kStBounceShift = 16;      // 8 bits
+constexpr uint32_t kStSpecular = 1u << 24;
+constexpr uint32_t kStCont = 1u << 25;       // continuation ray pending
+constexpr uint32_t kStNee = 1u << 26;        // NEE payload pending
+constexpr uint32_t kStDimOverflow = 1u << 27;
+
+// NEE payload layout (floats, stride n)
+constexpr int kNee = 16;
+constexpr int kNeeBeta = 0;    // 3: beta at the vertex
+constexpr int kNeeF = 3;       // 3: f*|cos| (portal kinds) or c1 (MIS light part)
+constexpr int kNeePdf = 6;     // portal-kind sampling pdf
+constexpr int kNeeLi = 7;      // 3: Li fallback on miss (portal kinds) / f2 (MIS)
+constexpr int kNeeSw = 10;     // MIS scattering weight
+constexpr int kNeeSpdf = 11;   // MIS scattering pdf
+constexpr int kNeeLpdf = 12;   // light selection pdf (UniformSampleOneLight)
+constexpr int kNeePortalPdf = 13;
+constexpr int kNeeLight = 14;  // light index (int bits)
+constexpr int kNeeFlags = 15;  // kNf* (int bits)
+
+constexpr uint32_t kNfPortal = 1u;     // portal-light estimator (ray A closest)
+constexpr uint32_t kNfMis = 2u;        // standard MIS (ray A shadow, ray B closest)
+constexpr uint32_t kNfA = 4u;          // ray A traced
+constexpr uint32_t kNfB = 8u;          // ray B traced
+constexpr uint32_t kNfDivPortal = 16u; // divide by portal pdf (projection strategy)
+constexpr uint32_t kNfC1 = 32u;        // MIS light contribution present (needs unoccluded A)
+
+// Ray queue entry kinds (low 2 bits)
+constexpr uint32_t kRayCont = 0, kRayA = 1, kRayShadow = 2, kRayB = 3;
+
+struct DevStats {
+    unsigned long long closest;
+    unsigned long long shadow;
+    unsigned long long nodes;
+    unsigned long long prims;
+    unsigned long long dim_overflow;
+    unsigned long long pad[3];
+};
+
+}  // namespace pt

@@ -1,0 +1,69 @@
+// host_common.h -- host-side declarations shared by the loader, the BVH
+// builder and the render driver.
+#pragma once
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pt.h"
+#include "ptmath.h"
+
+namespace pt {
+
+// Error carried to the C ABI boundary (converted to pt_status there).
+struct PtError : std::runtime_error {
+    pt_status status;
+    PtError(pt_status s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+// Host Matrix4x4 / Transform (src/core/transform.{h,cpp})
+struct HM4 {
+    float m[4][4];
+};
+struct HXF {
+    HM4 m, mi;
+};
+HM4 hm4_identity();
+HM4 hm4_mul(const HM4& a, const HM4& b);
+bool hm4_inverse(const HM4& m, HM4* out);
+HXF hxf_identity();
+HXF hxf_from_matrix(const HM4& m);
+HXF hxf_inverse(const HXF& t);
+HXF hxf_mul(const HXF& a, const HXF& b);
+HXF hxf_translate(float x, float y, float z);
+HXF hxf_scale(float x, float y, float z);
+HXF hxf_perspective(float fov, float n, float f);
+bool hxf_swaps_handedness(const HXF& t);
+M4 to_m4(const HM4& h);
+
+// Loader
+struct pt_host_scene_impl;
+pt_host_scene_impl* load_pbrt_file(const char* path);
+const pt_scene_desc* host_scene_desc(const pt_host_scene_impl* hs);
+void host_scene_free(pt_host_scene_impl* hs);
+
+// Axis-aligned box (Bounds3f)
+struct BBox {
+    V3 pmin, pmax;
+};
+
+// Flattened BVH (bvh.cpp:95-104 LinearBVHNode, 32 bytes)
+struct LinearNode {
+    float bmin[3];
+    float bmax[3];
+    int32_t offset;      // primitivesOffset (leaf) / secondChildOffset (interior)
+    uint16_t nprims;
+    uint8_t axis;
+    uint8_t pad;
+};
+static_assert(sizeof(LinearNode) == 32, "LinearBVHNode must be 32 bytes");
+
+// SAH BVH build over the scene's primitives (bvh.cpp:190-402, 640-658).
+// prim_order[i] = index into desc->prims of the i-th primitive in BVH order.
+void build_bvh(const pt_scene_desc* d, std::vector<LinearNode>* nodes, std::vector<int>* prim_order);
+
+// World bound of primitive i of desc->prims.
+BBox prim_world_bound(const pt_scene_desc* d, int i);
+
+}  // namespace pt

@@ -1,0 +1,31 @@
+// kernels.h -- launch geometry and small constant blocks shared by the
+// wavefront kernels and the host driver.
+#pragma once
+
+#include "device.h"
+
+namespace pt {
+
+constexpr int kTraceBlock = 128;  // 2 waves; LDS stack = kStackLds * 128 * 4 B
+constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
+constexpr int kShadeBlock = 128;
+constexpr int kMaxPortals = 64;
+
+// HaltonSampler constants for the per-pixel offset (halton.cpp:65-93)
+struct HaltonPixelConsts {
+    int exp1;
+    uint32_t scale0;
+    uint32_t mi0, mi1;
+};
+
+// Film constants (film.cpp:45-86, film.h:121-161)
+struct FilmConsts {
+    int crop_x0, crop_y0, crop_x1, crop_y1;
+    int sb_x0, sb_y0, sb_x1, sb_y1;
+    int win;  // filter window half-size in pixels
+    float rx, ry, inv_rx, inv_ry;
+    float max_lum;
+    float table[256];
+};
+
+}  // namespace pt

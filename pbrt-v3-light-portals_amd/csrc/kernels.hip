@@ -1,0 +1,677 @@
+// kernels.hip -- the wavefront path tracer's gfx950 kernels.
+//
+// One batch = (pixel list) x (consecutive sample indices).  Per bounce the
+// host enqueues k_trace over the ray queue (continuation + NEE rays) and
+// k_shade over the path queue.  k_shade first resolves the NEE rays of the
+// previous vertex (L += beta * Ld, integrator.cpp:122), then shades the new
+// hit exactly as PathIntegrator::Li (path.cpp:81-186) and appends the next
+// rays / live paths with one wave-aggregated atomic per wave (ballot +
+// mbcnt prefix).  k_film adds the finished samples to the film in sample
+// order (FilmTile::AddSample, film.h:121-161) by gathering over each pixel's
+// filter window -- deterministic, no float atomics.
+#include "devfuncs.h"
+#include "kernels.h"
+
+namespace pt {
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Reserve `cnt` (0..3) consecutive queue entries per lane with one atomic per
+// wave.  Must be reached by every active lane of the wave together.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter, uint32_t cnt) {
+    const uint64_t b0 = __ballot((cnt & 1u) != 0);
+    const uint64_t b1 = __ballot((cnt & 2u) != 0);
+    const uint64_t act = __ballot(1);
+    const uint32_t lane = lane_id();
+    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t prefix = (uint32_t)__popcll(b0 & lower) + 2u * (uint32_t)__popcll(b1 & lower);
+    const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1);
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader && total) base = atomicAdd(counter, total);
+    base = (uint32_t)__shfl((int)base, leader);
+    return base + prefix;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ void flush_stats(DevStats* s, unsigned long long cl, unsigned long long sh,
+                                            unsigned long long nodes, unsigned long long prims) {
+    cl = wave_sum_u64(cl);
+    sh = wave_sum_u64(sh);
+    nodes = wave_sum_u64(nodes);
+    prims = wave_sum_u64(prims);
+    if (lane_id() == 0) {
+        if (cl) atomicAdd(&s->closest, cl);
+        if (sh) atomicAdd(&s->shadow, sh);
+        if (nodes) atomicAdd(&s->nodes, nodes);
+        if (prims) atomicAdd(&s->prims, prims);
+    }
+}
+
+// ----------------------------------------------------------------------------
+// BVH traversal (BVHAccel::Intersect / IntersectP, bvh.cpp:662-738).
+// Near-child-first order by dirIsNeg[axis], tMax shrinking on every
+// accepted hit (GeometricPrimitive::Intersect, primitive.cpp:116-130).
+// The 64-entry node stack lives in LDS (kStackLds entries per lane,
+// [entry][lane] layout) with a per-thread global spill for deeper trees.
+// ----------------------------------------------------------------------------
+template <bool kAny>
+__device__ __forceinline__ int traverse(const DevScene& sc, Ray ray, int (*stk)[kTraceBlock], int* spill,
+                                        unsigned long long* nodes, unsigned long long* prims) {
+    const int tid = threadIdx.x;
+    const V3 inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+    const bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
+    const float kx = 1 + 2 * gammaf(3);
+    int toVisit = 0, cur = 0, hitPrim = -1;
+    if (sc.n_nodes == 0) return -1;
+    for (;;) {
+        const float4 a = sc.nodes[2 * cur];
+        const float4 b = sc.nodes[2 * cur + 1];
+        ++*nodes;
+        // Bounds3::IntersectP(ray, invDir, dirIsNeg) (geometry.h:1584-1606)
+        float tMin = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
+        float tMax = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
+        float tyMin = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
+        float tyMax = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
+        tMax *= kx;
+        tyMax *= kx;
+        bool hitb = !(tMin > tyMax || tyMin > tMax);
+        if (hitb) {
+            if (tyMin > tMin) tMin = tyMin;
+            if (tyMax < tMax) tMax = tyMax;
+            float tzMin = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
+            float tzMax = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
+            tzMax *= kx;
+            hitb = !(tMin > tzMax || tzMin > tMax);
+            if (hitb) {
+                if (tzMin > tMin) tMin = tzMin;
+                if (tzMax < tMax) tMax = tzMax;
+                hitb = (tMin < ray.tmax) && (tMax > 0);
+            }
+        }
+        if (hitb) {
+            const int off = __float_as_int(b.z);
+            const uint32_t npax = __float_as_uint(b.w);
+            const int np = (int)(npax & 0xffffu);
+            if (np > 0) {
+                for (int i = 0; i < np; ++i) {
+                    const int pi = off + i;
+                    ++*prims;
+                    const float4 r0 = sc.prims[3 * pi];
+                    const float4 r1 = sc.prims[3 * pi + 1];
+                    const uint32_t fl = __float_as_uint(r0.w);
+                    float t;
+                    bool ok;
+                    if (fl & kPrimPlane) {
+                        V3 ph;
+                        ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+                    } else {
+                        const float4 r2 = sc.prims[3 * pi + 2];
+                        float b0, b1, b2;
+                        ok = tri_test(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t, &b0,
+                                      &b1, &b2);
+                        if (!kAny && (fl & kPrimDegenerate)) ok = false;
+                    }
+                    if (ok) {
+                        if (kAny) return pi;
+                        ray.tmax = t;
+                        hitPrim = pi;
+                    }
+                }
+                if (toVisit == 0) break;
+                --toVisit;
+                cur = toVisit < kStackLds ? stk[toVisit][tid] : spill[toVisit - kStackLds];
+            } else {
+                const int axis = (int)(npax >> 16);
+                const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                const int far = neg ? cur + 1 : off;
+                cur = neg ? off : cur + 1;
+                if (toVisit < kStackLds) stk[toVisit][tid] = far;
+                else spill[toVisit - kStackLds] = far;
+                ++toVisit;
+            }
+        } else {
+            if (toVisit == 0) break;
+            --toVisit;
+            cur = toVisit < kStackLds ? stk[toVisit][tid] : spill[toVisit - kStackLds];
+        }
+    }
+    return hitPrim;
+}
+
+__device__ __forceinline__ Ray load_ray6(const float* a, uint32_t n, uint32_t slot, float tmax) {
+    return Ray{v3(a[slot], a[n + slot], a[2 * n + slot]), v3(a[3 * n + slot], a[4 * n + slot], a[5 * n + slot]), tmax};
+}
+__device__ __forceinline__ void store_ray6(float* a, uint32_t n, uint32_t slot, const Ray& r) {
+    a[slot] = r.o.x; a[n + slot] = r.o.y; a[2 * n + slot] = r.o.z;
+    a[3 * n + slot] = r.d.x; a[4 * n + slot] = r.d.y; a[5 * n + slot] = r.d.z;
+}
+
+__global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+                                                       const uint32_t* __restrict__ rq_count, int* spill,
+                                                       DevStats* stats) {
+    __shared__ int stk[kStackLds][kTraceBlock];
+    const uint32_t n = *rq_count;
+    const uint32_t N = (uint32_t)ps.n;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    int* myspill = spill + (size_t)gtid * (64 - kStackLds);
+    unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0;
+    for (uint32_t i = gtid; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t e = rq[i];
+        const uint32_t slot = e >> 2, kind = e & 3u;
+        if (kind == kRayShadow) {
+            const float* a = ps.rayA;
+            Ray r{v3(a[slot], a[N + slot], a[2 * N + slot]), v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
+                  a[6 * N + slot]};
+            int h = traverse<true>(sc, r, stk, myspill, &nodes, &prims);
+            ps.hitA[slot] = h >= 0 ? 1 : 0;
+            ++nsh;
+        } else {
+            Ray r;
+            if (kind == kRayCont) r = load_ray6(ps.ray, N, slot, kInf);
+            else if (kind == kRayA) r = load_ray6(ps.rayA, N, slot, kInf);
+            else r = load_ray6(ps.rayB, N, slot, kInf);
+            int h = traverse<false>(sc, r, stk, myspill, &nodes, &prims);
+            if (kind == kRayCont) ps.hit[slot] = h;
+            else if (kind == kRayA) ps.hitA[slot] = h;
+            else ps.hitB[slot] = h;
+            ++ncl;
+        }
+    }
+    flush_stats(stats, ncl, nsh, nodes, prims);
+}
+
+// ----------------------------------------------------------------------------
+// Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
+// (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ Ray camera_ray(const DevScene& sc, float fx, float fy, float lx, float ly) {
+    V3 pc = xf_point(sc.r2c, v3(fx, fy, 0));
+    Ray r{v3(0, 0, 0), normalize(v3(pc.x, pc.y, pc.z)), kInf};
+    if (sc.lens_radius > 0) {
+        float dx, dy;
+        concentric_sample_disk(lx, ly, &dx, &dy);
+        float plx = sc.lens_radius * dx, ply = sc.lens_radius * dy;
+        float ft = sc.focal_distance / r.d.z;
+        V3 pFocus = r.o + r.d * ft;
+        r.o = v3(plx, ply, 0);
+        r.d = normalize(pFocus - r.o);
+    }
+    return xf_ray(sc.c2w, r);
+}
+
+__global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const int2* __restrict__ pix, int npix,
+                                                int s0, int nsamp, HaltonPixelConsts hp, uint32_t* rq,
+                                                uint32_t* pq) {
+    const uint32_t N = (uint32_t)ps.n;
+    const uint32_t total = (uint32_t)npix * (uint32_t)nsamp;
+    for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
+        const uint32_t sl = slot / (uint32_t)npix, p = slot - sl * (uint32_t)npix;
+        const int2 px = pix[p];
+        const uint32_t off = halton_pixel_offset(sc, px.x, px.y, hp.exp1, hp.scale0, hp.mi0, hp.mi1);
+        const uint32_t idx = off + (uint32_t)(s0 + (int)sl) * sc.hal_stride;
+        const float fx = (float)px.x + halton_dim(sc, idx, 0);
+        const float fy = (float)px.y + halton_dim(sc, idx, 1);
+        float lx = 0.5f, ly = 0.5f;
+        if (sc.lens_radius > 0) { lx = halton_dim(sc, idx, 3); ly = halton_dim(sc, idx, 4); }
+        const Ray r = camera_ray(sc, fx, fy, lx, ly);
+        ps.hidx[slot] = idx;
+        ps.pfilm[slot] = make_float2(fx, fy);
+        ps.L[slot] = 0.f; ps.L[N + slot] = 0.f; ps.L[2 * N + slot] = 0.f;
+        ps.beta[slot] = 1.f; ps.beta[N + slot] = 1.f; ps.beta[2 * N + slot] = 1.f;
+        ps.eta[slot] = 1.f;
+        ps.st[slot] = 6u | kStCont;  // dims 0-5 consumed (pFilm, time, pLens, wvl)
+        store_ray6(ps.ray, N, slot, r);
+        rq[slot] = slot << 2 | kRayCont;
+        pq[slot] = slot;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Shading
+// ----------------------------------------------------------------------------
+struct Dims {
+    const DevScene* sc;
+    uint32_t idx;
+    int dim;
+    bool overflow;
+    __device__ __forceinline__ float get1() {
+        if (dim >= sc->max_dim) { overflow = true; ++dim; return 0.5f; }
+        return halton_dim(*sc, idx, dim++);
+    }
+};
+
+__device__ __forceinline__ S3 load_s3(const float* a, uint32_t n, uint32_t slot) {
+    return s3(a[slot], a[n + slot], a[2 * n + slot]);
+}
+__device__ __forceinline__ void store_s3(float* a, uint32_t n, uint32_t slot, S3 v) {
+    a[slot] = v.c[0]; a[n + slot] = v.c[1]; a[2 * n + slot] = v.c[2];
+}
+
+// Le of whatever area light the primitive carries (SurfaceInteraction::Le,
+// interaction.cpp:148-151); the hit normal is only needed for one-sided lights.
+__device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ray, int* lightOut) {
+    int mat, light;
+    prim_info(sc, prim, &mat, &light);
+    *lightOut = light;
+    if (light < 0) return s3(0.f);
+    const DevLight& l = sc.lights[light];
+    if (l.two_sided) return l.L;
+    SurfHit si;
+    if (!surface_at(sc, prim, ray, &si)) return s3(0.f);
+    return area_L(l, si.n, -ray.d);
+}
+
+// Finish the NEE of the previous vertex: Ld from the traced rays, then
+// L += beta * Ld / lightPdf (integrator.cpp:121, path.cpp:122-127).
+__device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, S3* L) {
+    const uint32_t N = (uint32_t)ps.n;
+    const float* nee = ps.nee;
+    const uint32_t fl = __float_as_uint(nee[kNeeFlags * N + slot]);
+    S3 Ld = s3(0.f);
+    if (fl & kNfPortal) {
+        if (fl & kNfA) {
+            S3 Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+            const int h = ps.hitA[slot];
+            if (h >= 0) {
+                int lid;
+                Li = hit_Le(sc, h, load_ray6(ps.rayA, N, slot, kInf), &lid);
+            }
+            const S3 f = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
+            if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / nee[kNeePdf * N + slot];
+        }
+        if (fl & kNfDivPortal) Ld = Ld / nee[kNeePortalPdf * N + slot];
+    } else if (fl & kNfMis) {
+        if ((fl & kNfC1) && ps.hitA[slot] == 0)
+            Ld = Ld + s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
+        if (fl & kNfB) {
+            const int h = ps.hitB[slot];
+            S3 Li = s3(0.f);
+            if (h >= 0) {
+                int lid;
+                const S3 le = hit_Le(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
+                if (lid == __float_as_int(nee[kNeeLight * N + slot])) Li = le;
+            }
+            if (!is_black(Li)) {
+                const S3 f2 = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+                Ld = Ld + (((f2 * Li) * s3(1.f)) * nee[kNeeSw * N + slot]) / nee[kNeeSpdf * N + slot];
+            }
+        }
+    }
+    const S3 bv = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
+    *L = *L + bv * (Ld / nee[kNeeLpdf * N + slot]);
+}
+
+__device__ __forceinline__ void put_nee(const DevPaths& ps, uint32_t slot, int k, float v) {
+    ps.nee[(uint32_t)k * (uint32_t)ps.n + slot] = v;
+}
+__device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int k, S3 v) {
+    put_nee(ps, slot, k, v.c[0]); put_nee(ps, slot, k + 1, v.c[1]); put_nee(ps, slot, k + 2, v.c[2]);
+}
+
+// PortalArealight::EstimateDirect set-up (portal_arealight.cpp:29-239).
+// u1 = uScattering (argument order at integrator.cpp:132); u2 is unused; the
+// selected portal is call-local.  Returns true when ray A was emitted.
+__device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
+                                           const SurfHit& it, const Bsdf& bsdf, float u10, float u11) {
+    const DevLight& l = sc.lights[lightIdx];
+    const DevPlane& lp = sc.planes[l.shape];
+    const uint32_t N = (uint32_t)ps.n;
+    uint32_t flags = kNfPortal;
+    if (l.strategy != PT_PORTAL_LIGHT) {
+        const V3 pObj = xf_point(lp.w2o, it.p);
+        float dist[kMaxPortals];
+        float sum = 0;
+        bool behindAll = true;
+        for (int i = 0; i < l.n_portals; ++i) {
+            if (!plane_in_front(sc.portal_planes[l.first_portal + i], pObj)) { dist[i] = 0; continue; }
+            behindAll = false;
+            dist[i] = 1;  // InFrustum() is always true (aaportal.cpp:101-104)
+            sum += dist[i];
+        }
+        if (!behindAll) {
+            if (sum == 0) { put_nee(ps, slot, kNeeFlags, __uint_as_float(flags)); return false; }
+            const int np = l.n_portals;
+            for (int i = 0; i < np; ++i) dist[i] /= sum;
+            float cdf[kMaxPortals + 1];
+            cdf[0] = 0;
+            for (int i = 1; i < np + 1; ++i) cdf[i] = cdf[i - 1] + dist[i - 1] / np;
+            const float funcInt = cdf[np];
+            if (funcInt == 0) { for (int i = 1; i < np + 1; ++i) cdf[i] = (float)i / (float)np; }
+            else { for (int i = 1; i < np + 1; ++i) cdf[i] /= funcInt; }
+            const int sel = find_interval(cdf, np + 1, u10);
+            const float portalPdf = (funcInt > 0) ? dist[sel] / (funcInt * np) : 0;
+            const DevPlane& pp = sc.portal_planes[l.first_portal + sel];
+            if (plane_in_front(pp, pObj)) {
+                V3 wi = v3(0, 0, 0);
+                float pdf = 0;
+                if (l.strategy == PT_PORTAL_UNIFORM) {
+                    // AAPortal::SamplePortal (aaportal.cpp:73-83)
+                    V3 sp, sn, spe;
+                    float areaPdf;
+                    plane_sample(pp, u10, u11, &sp, &sn, &spe, &areaPdf);
+                    wi = normalize(sp - it.p);
+                    pdf = dist2(it.p, sp) / (absdot(plane_normal(pp), -wi) * pp.area);
+                } else {
+                    // AAPortal::SampleProj (aaportal.cpp:114-159), literal
+                    const V3 dLo = normalize(it.p - lp.lo);
+                    const V3 dHi = normalize(it.p - lp.hi);
+                    if (dLo.z == 0 || dHi.z == 0) pdf = 0;
+                    else {
+                        const float tLo = (pp.lo[pp.ax] - lp.lo[lp.ax]) / dLo[lp.ax];
+                        const float tHi = (pp.lo[pp.ax] - lp.hi[lp.ax]) / dHi[lp.ax];
+                        const V3 projLo = lp.lo + dLo * tLo;
+                        const V3 projHi = lp.hi + dHi * tHi;
+                        const V3 isectHi = vmax(pp.lo, projLo);
+                        const V3 isectLo = vmin(pp.hi, projHi);
+                        const float len0 = isectHi[pp.ax0] - isectLo[pp.ax0];
+                        const float len1 = isectHi[pp.ax1] - isectLo[pp.ax1];
+                        V3 sampled = v3(0, 0, 0);
+                        sampled.set(pp.ax, pp.lo[pp.ax]);
+                        sampled.set(pp.ax0, isectLo[pp.ax0] + u10 * len0);
+                        sampled.set(pp.ax1, isectLo[pp.ax1] + u10 * len1);
+                        const V3 sampledWorld = xf_point(pp.w2o, sampled);
+                        wi = sampledWorld - it.p;
+                        pdf = dist2(it.p, sampled) / (absdot(plane_normal(pp), -wi) * (len0 * len1));
+                    }
+                    flags |= kNfDivPortal;
+                    put_nee(ps, slot, kNeePortalPdf, portalPdf);
+                }
+                if (pdf > 0) {
+                    const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
+                    store_ray6(ps.rayA, N, slot, r);
+                    put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn));
+                    put_nee(ps, slot, kNeePdf, pdf);
+                    put_nee3(ps, slot, kNeeLi, s3(0.f));
+                    flags |= kNfA;
+                }
+                put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+                return (flags & kNfA) != 0;
+            }
+        }
+    }
+    // EstimateDirectLight (portal_arealight.cpp:115-156)
+    V3 wi, sp, sn, spe;
+    float pdf = 0;
+    const S3 Li = area_sample_li(sc, l, it, u10, u11, &wi, &pdf, &sp, &sn, &spe);
+    if (!is_black(Li) && pdf > 0) {
+        const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
+        store_ray6(ps.rayA, N, slot, r);
+        put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn));
+        put_nee(ps, slot, kNeePdf, pdf);
+        put_nee3(ps, slot, kNeeLi, Li);
+        flags |= kNfA;
+    }
+    put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+    return (flags & kNfA) != 0;
+}
+
+// EstimateDirect, MIS branch (integrator.cpp:137-258) for a DiffuseAreaLight.
+// Emits ray A (shadow, any-hit) and/or ray B (BSDF-sampled, closest-hit).
+__device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
+                                            const SurfHit& it, const Bsdf& bsdf, float ul0, float ul1, float us0,
+                                            float us1) {
+    const DevLight& l = sc.lights[lightIdx];
+    const uint32_t N = (uint32_t)ps.n;
+    uint32_t flags = kNfMis;
+    V3 wi, sp, sn, spe;
+    float lightPdf = 0, scatteringPdf = 0;
+    const S3 Li = area_sample_li(sc, l, it, ul0, ul1, &wi, &lightPdf, &sp, &sn, &spe);
+    if (lightPdf > 0 && !is_black(Li)) {
+        const S3 f = bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn);
+        scatteringPdf = bsdf_pdf(bsdf, it.wo, wi);
+        if (!is_black(f)) {
+            // VisibilityTester::Unoccluded -> SpawnRayTo(Interaction) (light.cpp:59-61, interaction.h:75-80)
+            const V3 origin = offset_ray_origin(it.p, it.perr, it.n, sp - it.p);
+            const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
+            const V3 d = target - origin;
+            float* a = ps.rayA;
+            a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
+            a[3 * N + slot] = d.x; a[4 * N + slot] = d.y; a[5 * N + slot] = d.z;
+            a[6 * N + slot] = 1 - kShadowEps;
+            const float lightWeight = power_heuristic(lightPdf, scatteringPdf);
+            put_nee3(ps, slot, kNeeF, ((f * Li) * lightWeight) / lightPdf);
+            flags |= kNfA | kNfC1;
+        }
+    }
+    {
+        float pdf2 = scatteringPdf;
+        V3 wi2 = wi;
+        S3 f = bsdf_sample(bsdf, it.wo, &wi2, us0, us1, &pdf2);
+        f = f * absdot(wi2, it.sn);
+        if (!is_black(f) && pdf2 > 0) {
+            const float lp = area_pdf_li(sc, l, it, wi2);
+            if (lp != 0) {
+                const float sw = power_heuristic(pdf2, lp);
+                const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi2), wi2, kInf};
+                store_ray6(ps.rayB, N, slot, r);
+                put_nee3(ps, slot, kNeeLi, f);
+                put_nee(ps, slot, kNeeSw, sw);
+                put_nee(ps, slot, kNeeSpdf, pdf2);
+                put_nee(ps, slot, kNeeLight, __int_as_float(lightIdx));
+                flags |= kNfB;
+            }
+        }
+    }
+    put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+    return flags;
+}
+
+// One path step.  Returns the rays to enqueue in rays[] and whether the path
+// stays alive.
+__device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
+                                           uint32_t* nrays, bool* keep, bool* overflow) {
+    const uint32_t N = (uint32_t)ps.n;
+    uint32_t st = ps.st[slot];
+    S3 L = load_s3(ps.L, N, slot);
+    *nrays = 0;
+    if (st & kStNee) {
+        resolve_nee(sc, ps, slot, &L);
+        st &= ~kStNee;
+    }
+    if (st & kStCont) {
+        st &= ~kStCont;
+        int bounces = (int)((st >> kStBounceShift) & 0xffu);
+        const bool specular = (st & kStSpecular) != 0;
+        const Ray ray = load_ray6(ps.ray, N, slot, kInf);
+        const int hp = ps.hit[slot];
+        S3 beta = load_s3(ps.beta, N, slot);
+        SurfHit si;
+        bool found = hp >= 0 && surface_at(sc, hp, ray, &si);
+        int mat = -1, light = -1;
+        if (found) prim_info(sc, hp, &mat, &light);
+        if (bounces == 0 || specular) {
+            if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
+        }
+        if (found && bounces < sc.max_depth) {
+            const pt_material m = sc.mats[mat];
+            if (m.kind == PT_MAT_NONE) {
+                // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
+                const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
+                store_ray6(ps.ray, N, slot, r);
+                st |= kStCont;
+                rays[(*nrays)++] = slot << 2 | kRayCont;
+            } else {
+                Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+                Bsdf bsdf;
+                make_bsdf(m, si, &bsdf);
+                if (bsdf.nbxdf > 0) {
+                    // UniformSampleOneLight (integrator.cpp:100-122)
+                    bool deferred = false;
+                    float lightPdf = 0;
+                    bool haveLight = false;
+                    if (sc.n_lights > 0) {
+                        const float ul = dm.get1();
+                        const int ln = find_interval(sc.ldist_cdf, sc.n_lights + 1, ul);
+                        lightPdf = (sc.ldist_int > 0) ? sc.ldist_func[ln] / (sc.ldist_int * sc.n_lights) : 0;
+                        if (lightPdf != 0) {
+                            haveLight = true;
+                            const float uL0 = dm.get1(), uL1 = dm.get1();
+                            const float uS0 = dm.get1(), uS1 = dm.get1();
+                            if (sc.lights[ln].kind == PT_LIGHT_PORTAL_AREA) {
+                                if (portal_nee(sc, ps, slot, ln, si, bsdf, uS0, uS1)) {
+                                    rays[(*nrays)++] = slot << 2 | kRayA;
+                                    deferred = true;
+                                }
+                            } else {
+                                const uint32_t f = mis_nee(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1);
+                                if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
+                                if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
+                                deferred = (f & (kNfA | kNfB)) != 0;
+                            }
+                        }
+                    }
+                    if (deferred) {
+                        put_nee3(ps, slot, kNeeBeta, beta);
+                        put_nee(ps, slot, kNeeLpdf, lightPdf);
+                        st |= kStNee;
+                    } else {
+                        // no ray: EstimateDirect returned Spectrum(0)
+                        L = L + beta * (haveLight ? s3(0.f) / lightPdf : s3(0.f));
+                    }
+                }
+                // BSDF sampling (path.cpp:131-151)
+                const float u0 = dm.get1(), u1 = dm.get1();
+                V3 wi = v3(0, 0, 0);
+                float pdf = 0;
+                const S3 f = bsdf_sample(bsdf, -ray.d, &wi, u0, u1, &pdf);
+                if (!(is_black(f) || pdf == 0.f)) {
+                    beta = beta * ((f * absdot(wi, si.sn)) / pdf);
+                    st &= ~kStSpecular;
+                    const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
+                    bool alive = true;
+                    // Russian roulette (path.cpp:177-185)
+                    const S3 rrBeta = beta * ps.eta[slot];
+                    if (max_comp(rrBeta) < sc.rr_threshold && bounces > 3) {
+                        const float q = smax(0.05f, 1 - max_comp(rrBeta));
+                        if (dm.get1() < q) alive = false;
+                        else beta = beta / (1 - q);
+                    }
+                    if (alive) {
+                        store_ray6(ps.ray, N, slot, r);
+                        store_s3(ps.beta, N, slot, beta);
+                        ++bounces;
+                        st |= kStCont;
+                        rays[(*nrays)++] = slot << 2 | kRayCont;
+                    }
+                }
+                if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
+                st = (st & ~kStDimMask) | ((uint32_t)dm.dim & kStDimMask);
+                st = (st & ~(0xffu << kStBounceShift)) | ((uint32_t)(bounces & 0xff) << kStBounceShift);
+            }
+        }
+    }
+    store_s3(ps.L, N, slot, L);
+    ps.st[slot] = st;
+    *keep = (st & (kStCont | kStNee)) != 0;
+}
+
+__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
+                                                       const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                                       uint32_t* rq_out_count, uint32_t* pq_out,
+                                                       uint32_t* pq_out_count, DevStats* stats) {
+    const uint32_t n = *pq_count;
+    bool overflow = false;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t rays[3];
+        uint32_t nrays = 0;
+        bool keep = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = pq[i];
+            shade_path(sc, ps, slot, rays, &nrays, &keep, &overflow);
+        }
+        const uint32_t pos = wave_reserve(rq_out_count, nrays);
+        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
+        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
+        if (keep) pq_out[ppos] = slot;
+    }
+    if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
+}
+
+// ----------------------------------------------------------------------------
+// Film: gather the batch's samples into each pixel in sample order
+// (FilmTile::AddSample film.h:121-161 + the radiance sanitiser,
+// integrator.cpp:592-613).  Accumulates RGB contribution sums + weights.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int npix,
+                                              int nsamp, float4* accum) {
+    const int cw = fc.crop_x1 - fc.crop_x0, ch = fc.crop_y1 - fc.crop_y0;
+    const int total = cw * ch;
+    const uint32_t N = (uint32_t)ps.n;
+    const int sbw = fc.sb_x1 - fc.sb_x0;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const int tx = fc.crop_x0 + t % cw, ty = fc.crop_y0 + t / cw;
+        float4 acc = accum[t];
+        bool touched = false;
+        for (int sl = 0; sl < nsamp; ++sl) {
+            for (int qy = ty - fc.win; qy <= ty + fc.win; ++qy) {
+                if (qy < fc.sb_y0 || qy >= fc.sb_y1) continue;
+                for (int qx = tx - fc.win; qx <= tx + fc.win; ++qx) {
+                    if (qx < fc.sb_x0 || qx >= fc.sb_x1) continue;
+                    const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)];
+                    if (p < 0) continue;
+                    const uint32_t slot = (uint32_t)sl * (uint32_t)npix + (uint32_t)p;
+                    const float2 pf = ps.pfilm[slot];
+                    const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
+                    const int x0 = (int)ceilf(dx - fc.rx), x1 = (int)floorf(dx + fc.rx) + 1;
+                    const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
+                    if (tx < x0 || tx >= x1 || ty < y0 || ty >= y1) continue;
+                    S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                    if (has_nan(L)) L = s3(0.f);
+                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
+                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
+                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                    const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
+                    const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
+                    int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                    int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                    const float w = fc.table[iy * 16 + ix];
+                    const S3 c = (L * 1.f) * w;
+                    acc.x += c.c[0]; acc.y += c.c[1]; acc.z += c.c[2]; acc.w += w;
+                    touched = true;
+                }
+            }
+        }
+        if (touched) accum[t] = acc;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Test hooks (parity unit tests through the C ABI)
+// ----------------------------------------------------------------------------
+__global__ void k_debug_halton(DevScene sc, const uint32_t* idx, const int* dims, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = dims[i] < sc.max_dim ? halton_dim(sc, idx[i], dims[i]) : -1.f;
+}
+__global__ void k_debug_pixel_offset(DevScene sc, HaltonPixelConsts hp, const int2* pix, int n, uint32_t* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = halton_pixel_offset(sc, pix[i].x, pix[i].y, hp.exp1, hp.scale0, hp.mi0, hp.mi1);
+}
+__global__ void k_debug_camera(DevScene sc, const float* film, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r = camera_ray(sc, film[2 * i], film[2 * i + 1], 0.5f, 0.5f);
+    out[6 * i] = r.o.x; out[6 * i + 1] = r.o.y; out[6 * i + 2] = r.o.z;
+    out[6 * i + 3] = r.d.x; out[6 * i + 4] = r.d.y; out[6 * i + 5] = r.d.z;
+}
+__global__ __launch_bounds__(kTraceBlock) void k_debug_trace(DevScene sc, const float* rays, int n, int any,
+                                                             int* spill, int* out_prim) {
+    __shared__ int stk[kStackLds][kTraceBlock];
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r{v3(rays[7 * i], rays[7 * i + 1], rays[7 * i + 2]), v3(rays[7 * i + 3], rays[7 * i + 4], rays[7 * i + 5]),
+          rays[7 * i + 6]};
+    unsigned long long a = 0, b = 0;
+    int* sp = spill + (size_t)i * (64 - kStackLds);
+    out_prim[i] = any ? traverse<true>(sc, r, stk, sp, &a, &b) : traverse<false>(sc, r, stk, sp, &a, &b);
+}
+
+}  // namespace pt

@@ -1,0 +1,930 @@
+// render.hip -- host driver of the wavefront path tracer and the C ABI
+// (include/pt.h).  Replaces SamplerIntegrator::Render (integrator.cpp:
+// 526-637) for the PathIntegrator: the scene is flattened once into device
+// buffers, then the (pixel x sample) index space runs as batches of
+// independent paths through camera -> {trace, shade}* -> film kernels.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host_common.h"
+#include "kernels.hip"
+
+namespace pt {
+
+static thread_local std::string g_last_error;
+
+#define HIPCHK(x)                                                                                         \
+    do {                                                                                                  \
+        hipError_t e_ = (x);                                                                              \
+        if (e_ != hipSuccess) throw PtError(PT_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        if (count <= n && p) return;
+        release();
+        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, bytes);
+        if (e != hipSuccess) throw PtError(PT_ERR_OOM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+        p = (T*)q;
+        n = count;
+    }
+    void upload(const T* h, size_t count) {
+        alloc(count);
+        if (count) HIPCHK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+    }
+    void upload(const std::vector<T>& v) { upload(v.data(), v.size()); }
+};
+
+// ---------------------------------------------------------------------------
+// Halton tables (lowdiscrepancy.cpp:40-124, 2490-2504; halton.cpp:45-93)
+// ---------------------------------------------------------------------------
+struct HaltonTables {
+    std::vector<int> primes, prime_sums;
+    std::vector<uint16_t> perms;
+};
+static const HaltonTables& halton_tables() {
+    static HaltonTables t = [] {
+        HaltonTables h;
+        for (int c = 2; (int)h.primes.size() < 1000; ++c) {
+            bool ok = true;
+            for (int q : h.primes) {
+                if (q * q > c) break;
+                if (c % q == 0) { ok = false; break; }
+            }
+            if (ok) h.primes.push_back(c);
+        }
+        int s = 0;
+        for (int p : h.primes) { h.prime_sums.push_back(s); s += p; }
+        h.perms.resize((size_t)s);
+        // RNG in its default state (rng.h:129) and Shuffle (sampling.h:152-158)
+        uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+        auto next = [&]() {
+            uint64_t old = state;
+            state = old * 0x5851f42d4c957f2dULL + inc;
+            uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+            uint32_t rot = (uint32_t)(old >> 59u);
+            return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+        };
+        auto bounded = [&](uint32_t b) {
+            uint32_t threshold = (~b + 1u) % b;
+            for (;;) { uint32_t r = next(); if (r >= threshold) return r % b; }
+        };
+        uint16_t* p = h.perms.data();
+        for (int P : h.primes) {
+            for (int j = 0; j < P; ++j) p[j] = (uint16_t)j;
+            for (int j = 0; j < P; ++j) {
+                int other = j + (int)bounded((uint32_t)(P - j));
+                std::swap(p[j], p[other]);
+            }
+            p += P;
+        }
+        return h;
+    }();
+    return t;
+}
+
+static DivMagic make_div_magic(uint32_t d) {
+    DivMagic m{};
+    m.base = d;
+    m.inv_base = (float)1 / (float)d;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;  // ceil(log2 d)
+    m.magic = (uint32_t)((((unsigned __int128)1 << 32) * ((1ull << l) - d)) / d + 1);
+    m.shift = l - 1;
+    return m;
+}
+
+static void extended_gcd(uint64_t a, uint64_t b, int64_t* x, int64_t* y) {  // halton.cpp:51-61
+    if (b == 0) { *x = 1; *y = 0; return; }
+    int64_t d = (int64_t)(a / b), xp, yp;
+    extended_gcd(b, a % b, &xp, &yp);
+    *x = yp;
+    *y = xp - (d * yp);
+}
+static uint64_t mult_inverse(int64_t a, int64_t n) {
+    int64_t x, y;
+    extended_gcd((uint64_t)a, (uint64_t)n, &x, &y);
+    int64_t r = x - (x / n) * n;
+    return (uint64_t)(r < 0 ? r + n : r);
+}
+
+// ---------------------------------------------------------------------------
+// Device scene
+// ---------------------------------------------------------------------------
+struct Frame {
+    int crop_x0, crop_y0, crop_x1, crop_y1;
+    int sb_x0, sb_y0, sb_x1, sb_y1;
+    int pb_x0, pb_y0, pb_x1, pb_y1;  // integrator pixelBounds
+    int ntx, nty;
+    int width() const { return crop_x1 - crop_x0; }
+    int height() const { return crop_y1 - crop_y0; }
+};
+
+struct Work {
+    DBuf<uint32_t> hidx, st, rq0, rq1, pq0, pq1, counts;
+    DBuf<float2> pfilm;
+    DBuf<float> L, beta, eta, ray, rayA, rayB, nee;
+    DBuf<int> hit, hitA, hitB, spill;
+    DBuf<DevStats> stats;
+    size_t cap = 0;
+    void ensure(size_t n, size_t spill_threads) {
+        if (n > cap) {
+            hidx.alloc(n); st.alloc(n); rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
+            pfilm.alloc(n); L.alloc(3 * n); beta.alloc(3 * n); eta.alloc(n); ray.alloc(6 * n); rayA.alloc(7 * n);
+            rayB.alloc(6 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
+            cap = n;
+        }
+        spill.alloc(spill_threads * (64 - kStackLds));
+        counts.alloc(8);
+        stats.alloc(1);
+    }
+    DevPaths paths(int n) {
+        DevPaths p{};
+        p.n = n;
+        p.hidx = hidx.p; p.pfilm = pfilm.p; p.L = L.p; p.beta = beta.p; p.eta = eta.p; p.st = st.p;
+        p.ray = ray.p; p.hit = hit.p; p.rayA = rayA.p; p.hitA = hitA.p; p.rayB = rayB.p; p.hitB = hitB.p;
+        p.nee = nee.p;
+        return p;
+    }
+};
+
+}  // namespace pt
+
+struct pt_scene {
+    pt::DBuf<float4> nodes, prims;
+    pt::DBuf<pt_triangle> tris;
+    pt::DBuf<float> P, N, S, UV, lfunc, lcdf, tri_area, perm_c0;
+    pt::DBuf<pt::DevPlane> planes, pplanes;
+    pt::DBuf<pt_material> mats;
+    pt::DBuf<pt::DevLight> lights;
+    pt::DBuf<uint16_t> perm;
+    pt::DBuf<int> psums;
+    pt::DBuf<pt::DivMagic> divs;
+    pt::DevScene dev{};
+    pt::HaltonPixelConsts hpc{};
+    pt::FilmConsts film{};
+    pt::Frame fr{};
+    pt_film_desc filmdesc{};
+    int spp = 0;
+    std::vector<pt::LinearNode> host_nodes;
+    std::vector<int> host_prim_order;
+    pt::Work work;
+    int device = 0;
+    int num_cus = 256;
+    size_t target_slots = (size_t)8 << 20;
+};
+
+namespace pt {
+
+static int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+static void build_scene(pt_scene* s, const pt_scene_desc* d) {
+    if (!d) throw PtError(PT_ERR_INVALID_ARG, "null scene description");
+    if (d->n_prims < 0 || d->n_triangles < 0 || d->n_planes < 0 || d->n_lights < 0 || d->n_materials < 0)
+        throw PtError(PT_ERR_INVALID_ARG, "negative counts in scene description");
+    if (d->n_triangles > 0 && !d->P) throw PtError(PT_ERR_INVALID_ARG, "triangles without vertices");
+    for (int i = 0; i < d->n_prims; ++i) {
+        const pt_prim& p = d->prims[i];
+        if (p.kind == PT_PRIM_TRIANGLE) {
+            if (p.index < 0 || p.index >= d->n_triangles) throw PtError(PT_ERR_INVALID_ARG, "bad triangle prim");
+        } else if (p.kind == PT_PRIM_AAPLANE) {
+            if (p.index < 0 || p.index >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad plane prim");
+        } else
+            throw PtError(PT_ERR_INVALID_ARG, "bad prim kind");
+    }
+    for (int i = 0; i < d->n_triangles; ++i) {
+        const pt_triangle& t = d->triangles[i];
+        for (int k = 0; k < 3; ++k)
+            if (t.v[k] < 0 || t.v[k] >= d->n_vertices) throw PtError(PT_ERR_INVALID_ARG, "triangle vertex out of range");
+        if (t.material < 0 || t.material >= d->n_materials) throw PtError(PT_ERR_INVALID_ARG, "bad material index");
+        if (t.area_light >= d->n_lights) throw PtError(PT_ERR_INVALID_ARG, "bad light index");
+    }
+    for (int i = 0; i < d->n_planes; ++i) {
+        const pt_aaplane& p = d->planes[i];
+        if (p.axis < 0 || p.axis > 2) throw PtError(PT_ERR_INVALID_ARG, "bad plane axis");
+        if (p.material < 0 || p.material >= d->n_materials) throw PtError(PT_ERR_INVALID_ARG, "bad material index");
+    }
+    for (int i = 0; i < d->n_materials; ++i) {
+        int k = d->materials[i].kind;
+        if (k != PT_MAT_NONE && k != PT_MAT_MATTE) throw PtError(PT_ERR_UNSUPPORTED, "unsupported material kind");
+        if (k == PT_MAT_MATTE && d->materials[i].sigma != 0.f)
+            throw PtError(PT_ERR_UNSUPPORTED, "OrenNayar (sigma != 0) not supported");
+    }
+    for (int i = 0; i < d->n_lights; ++i) {
+        const pt_light& l = d->lights[i];
+        if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
+            if (l.shape < 0 || l.shape >= d->n_triangles) throw PtError(PT_ERR_INVALID_ARG, "bad light shape");
+        } else if (l.kind == PT_LIGHT_PORTAL_AREA) {
+            if (l.shape < 0 || l.shape >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad portal light shape");
+            if (l.n_portals < 0 || l.n_portals > kMaxPortals || l.first_portal < 0 ||
+                l.first_portal + l.n_portals > d->n_portals)
+                throw PtError(PT_ERR_INVALID_ARG, "bad portal range");
+        } else
+            throw PtError(PT_ERR_UNSUPPORTED, "unsupported light kind");
+    }
+    if (d->sampler.spp <= 0) throw PtError(PT_ERR_INVALID_ARG, "spp must be > 0");
+    if (d->film.xres <= 0 || d->film.yres <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad film resolution");
+    if (d->integrator.max_depth < 0 || d->integrator.max_depth > 250)
+        throw PtError(PT_ERR_UNSUPPORTED, "maxdepth must be in [0, 250]");
+
+    // ---- BVH (host build, reference order) ----
+    build_bvh(d, &s->host_nodes, &s->host_prim_order);
+    std::vector<float4> nodes(2 * s->host_nodes.size());
+    for (size_t i = 0; i < s->host_nodes.size(); ++i) {
+        const LinearNode& n = s->host_nodes[i];
+        nodes[2 * i] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
+        uint32_t npax = (uint32_t)n.nprims | ((uint32_t)n.axis << 16);
+        nodes[2 * i + 1] = make_float4(n.bmax[1], n.bmax[2], __builtin_bit_cast(float, n.offset),
+                                       __builtin_bit_cast(float, npax));
+    }
+    auto Pv = [&](int k) { return v3(d->P[3 * k], d->P[3 * k + 1], d->P[3 * k + 2]); };
+    std::vector<float4> prims(3 * s->host_prim_order.size());
+    for (size_t i = 0; i < s->host_prim_order.size(); ++i) {
+        const pt_prim& p = d->prims[s->host_prim_order[i]];
+        uint32_t flags = 0;
+        V3 a = v3(0, 0, 0), b = a, c = a;
+        if (p.kind == PT_PRIM_AAPLANE) {
+            flags = kPrimPlane;
+        } else {
+            const pt_triangle& t = d->triangles[p.index];
+            a = Pv(t.v[0]); b = Pv(t.v[1]); c = Pv(t.v[2]);
+            // Would Triangle::Intersect reject every ray after the t test?
+            // (triangle.cpp:297-318: degenerate dp/duv and zero geometric normal)
+            float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+            if ((t.flags & PT_TRI_HAS_UV) && d->UV)
+                for (int k = 0; k < 3; ++k) { uv[k][0] = d->UV[2 * t.v[k]]; uv[k][1] = d->UV[2 * t.v[k] + 1]; }
+            float duv02[2] = {uv[0][0] - uv[2][0], uv[0][1] - uv[2][1]};
+            float duv12[2] = {uv[1][0] - uv[2][0], uv[1][1] - uv[2][1]};
+            V3 dp02 = a - c, dp12 = b - c;
+            float det = duv02[0] * duv12[1] - duv02[1] * duv12[0];
+            bool degUV = std::fabs((double)det) < 1e-8;
+            V3 dpdu = v3(0, 0, 0), dpdv = v3(0, 0, 0);
+            if (!degUV) {
+                float inv = 1 / det;
+                dpdu = (duv12[1] * dp02 - duv02[1] * dp12) * inv;
+                dpdv = (-duv12[0] * dp02 + duv02[0] * dp12) * inv;
+            }
+            if (degUV || len2(cross(dpdu, dpdv)) == 0) {
+                if (len2(cross(c - a, b - a)) == 0) flags |= kPrimDegenerate;
+            }
+        }
+        prims[3 * i] = make_float4(a.x, a.y, a.z, __builtin_bit_cast(float, flags));
+        prims[3 * i + 1] = make_float4(b.x, b.y, b.z, __builtin_bit_cast(float, p.index));
+        prims[3 * i + 2] = make_float4(c.x, c.y, c.z, 0.f);
+    }
+    s->nodes.upload(nodes);
+    s->prims.upload(prims);
+    s->tris.upload(d->triangles, (size_t)d->n_triangles);
+    s->P.upload(d->P, (size_t)3 * d->n_vertices);
+    if (d->N) s->N.upload(d->N, (size_t)3 * d->n_vertices);
+    if (d->S) s->S.upload(d->S, (size_t)3 * d->n_vertices);
+    if (d->UV) s->UV.upload(d->UV, (size_t)2 * d->n_vertices);
+
+    // ---- triangle areas (triangle.cpp:576-582) ----
+    std::vector<float> area((size_t)d->n_triangles);
+    for (int i = 0; i < d->n_triangles; ++i) {
+        const pt_triangle& t = d->triangles[i];
+        V3 p0 = Pv(t.v[0]), p1 = Pv(t.v[1]), p2 = Pv(t.v[2]);
+        area[i] = (float)(0.5 * (double)len(cross(p1 - p0, p2 - p0)));
+    }
+    s->tri_area.upload(area);
+
+    // ---- planes and portals (plane.h:15-32, aaportal.cpp:8-13) ----
+    auto make_plane = [&](const float* lo, const float* hi, int axis, bool ro, bool sh, const pt_transform& o2w,
+                          int material, int light) {
+        DevPlane pl{};
+        pl.lo = v3(lo[0], lo[1], lo[2]);
+        pl.hi = v3(hi[0], hi[1], hi[2]);
+        pl.ax = axis;
+        pl.ax0 = axis == 2 ? 0 : (axis == 0 ? 1 : 2);
+        pl.ax1 = axis == 2 ? 1 : (axis == 0 ? 2 : 0);
+        pl.facing_fw = ro ? 0 : 1;
+        pl.ro_xor_sh = (ro != sh) ? 1 : 0;
+        pl.material = material;
+        pl.area_light = light;
+        std::memcpy(pl.o2w.m, o2w.m, 64);
+        std::memcpy(pl.w2o.m, o2w.minv, 64);
+        V3 loW = xf_point(pl.o2w, pl.lo), hiW = xf_point(pl.o2w, pl.hi);
+        pl.area = (hiW[pl.ax0] - loW[pl.ax0]) * (hiW[pl.ax1] - loW[pl.ax1]);
+        return pl;
+    };
+    std::vector<DevPlane> planes;
+    for (int i = 0; i < d->n_planes; ++i) {
+        const pt_aaplane& p = d->planes[i];
+        planes.push_back(make_plane(p.lo, p.hi, p.axis, (p.flags & PT_TRI_REVERSE_ORIENTATION) != 0,
+                                    (p.flags & PT_TRI_SWAPS_HANDEDNESS) != 0, p.object_to_world, p.material,
+                                    p.area_light));
+    }
+    std::vector<DevPlane> pplanes((size_t)d->n_portals);
+    std::vector<DevLight> lights;
+    for (int i = 0; i < d->n_lights; ++i) {
+        const pt_light& l = d->lights[i];
+        DevLight dl{};
+        dl.kind = l.kind;
+        dl.L = s3(l.L[0], l.L[1], l.L[2]);
+        dl.two_sided = l.two_sided;
+        dl.shape = l.shape;
+        dl.strategy = l.strategy;
+        dl.first_portal = l.first_portal;
+        dl.n_portals = l.n_portals;
+        if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
+        else {
+            dl.area = planes[l.shape].area;
+            const pt_aaplane& lp = d->planes[l.shape];
+            for (int k = 0; k < l.n_portals; ++k) {
+                const pt_portal& po = d->portals[l.first_portal + k];
+                pplanes[l.first_portal + k] = make_plane(po.lo, po.hi, po.axis, !po.facing_fw,
+                                                         (lp.flags & PT_TRI_SWAPS_HANDEDNESS) != 0,
+                                                         lp.object_to_world, -1, -1);
+            }
+        }
+        lights.push_back(dl);
+    }
+    s->planes.upload(planes);
+    s->pplanes.upload(pplanes);
+    s->lights.upload(lights);
+    s->mats.upload(d->materials, (size_t)d->n_materials);
+
+    // ---- light selection distribution (lightdistrib.cpp:68-75, integrator.cpp:515-522) ----
+    int nl = d->n_lights;
+    std::vector<float> func((size_t)std::max(nl, 1), 1.f), cdf((size_t)nl + 2, 0.f);
+    float funcInt = 0;
+    if (nl > 0) {
+        if (d->integrator.light_strategy == PT_LIGHTS_POWER && nl > 1) {
+            for (int i = 0; i < nl; ++i) {
+                const DevLight& l = lights[i];
+                S3 pw = ((l.L * (float)(l.two_sided ? 2 : 1)) * l.area) * kPi;  // DiffuseAreaLight::Power
+                func[i] = lum_y(pw);
+            }
+        }
+        cdf[0] = 0;
+        for (int i = 1; i < nl + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] / nl;
+        funcInt = cdf[nl];
+        if (funcInt == 0) { for (int i = 1; i < nl + 1; ++i) cdf[i] = (float)i / (float)nl; }
+        else { for (int i = 1; i < nl + 1; ++i) cdf[i] /= funcInt; }
+    }
+    s->lfunc.upload(func);
+    s->lcdf.upload(cdf);
+
+    // ---- film (film.cpp:45-86) ----
+    const pt_film_desc& f = d->film;
+    Frame& fr = s->fr;
+    fr.crop_x0 = (int)std::ceil((float)f.xres * f.crop[0]);
+    fr.crop_y0 = (int)std::ceil((float)f.yres * f.crop[2]);
+    fr.crop_x1 = (int)std::ceil((float)f.xres * f.crop[1]);
+    fr.crop_y1 = (int)std::ceil((float)f.yres * f.crop[3]);
+    if (fr.crop_x1 <= fr.crop_x0 || fr.crop_y1 <= fr.crop_y0) throw PtError(PT_ERR_INVALID_ARG, "empty crop window");
+    float rx = f.filter_radius[0], ry = f.filter_radius[1];
+    if (!(rx > 0) || !(ry > 0)) throw PtError(PT_ERR_INVALID_ARG, "filter radius must be > 0");
+    fr.sb_x0 = (int)std::floor((float)fr.crop_x0 + 0.5f - rx);
+    fr.sb_y0 = (int)std::floor((float)fr.crop_y0 + 0.5f - ry);
+    fr.sb_x1 = (int)std::ceil((float)fr.crop_x1 - 0.5f + rx);
+    fr.sb_y1 = (int)std::ceil((float)fr.crop_y1 - 0.5f + ry);
+    fr.pb_x0 = fr.sb_x0; fr.pb_y0 = fr.sb_y0; fr.pb_x1 = fr.sb_x1; fr.pb_y1 = fr.sb_y1;
+    if (d->integrator.has_pixel_bounds) {
+        const int* pb = d->integrator.pixel_bounds;
+        fr.pb_x0 = std::max(fr.pb_x0, std::min(pb[0], pb[1]));
+        fr.pb_x1 = std::min(fr.pb_x1, std::max(pb[0], pb[1]));
+        fr.pb_y0 = std::max(fr.pb_y0, std::min(pb[2], pb[3]));
+        fr.pb_y1 = std::min(fr.pb_y1, std::max(pb[2], pb[3]));
+    }
+    fr.ntx = ceil_div(fr.sb_x1 - fr.sb_x0, 16);
+    fr.nty = ceil_div(fr.sb_y1 - fr.sb_y0, 16);
+    s->filmdesc = f;
+    FilmConsts& fc = s->film;
+    fc.crop_x0 = fr.crop_x0; fc.crop_y0 = fr.crop_y0; fc.crop_x1 = fr.crop_x1; fc.crop_y1 = fr.crop_y1;
+    fc.sb_x0 = fr.sb_x0; fc.sb_y0 = fr.sb_y0; fc.sb_x1 = fr.sb_x1; fc.sb_y1 = fr.sb_y1;
+    fc.rx = rx; fc.ry = ry;
+    fc.inv_rx = 1 / rx; fc.inv_ry = 1 / ry;
+    fc.win = (int)std::ceil(std::max(rx, ry) + 0.5f);
+    fc.max_lum = f.max_sample_luminance;
+    {
+        float expX = 0, expY = 0, alpha = f.gaussian_alpha;
+        if (f.filter == PT_FILTER_GAUSSIAN) {
+            expX = std::exp(-alpha * rx * rx);
+            expY = std::exp(-alpha * ry * ry);
+        } else if (f.filter != PT_FILTER_BOX)
+            throw PtError(PT_ERR_UNSUPPORTED, "unsupported filter");
+        int off = 0;
+        for (int y = 0; y < 16; ++y)
+            for (int x = 0; x < 16; ++x, ++off) {
+                float px = (x + 0.5f) * rx / 16, py = (y + 0.5f) * ry / 16;
+                if (f.filter == PT_FILTER_GAUSSIAN) {
+                    float gx = smax(0.f, (float)(std::exp(-alpha * px * px) - expX));
+                    float gy = smax(0.f, (float)(std::exp(-alpha * py * py) - expY));
+                    fc.table[off] = gx * gy;
+                } else
+                    fc.table[off] = 1.f;
+            }
+    }
+
+    // ---- Halton (halton.cpp:65-93) ----
+    const HaltonTables& ht = halton_tables();
+    int res[2] = {fr.sb_x1 - fr.sb_x0, fr.sb_y1 - fr.sb_y0};
+    int scales[2], exps[2];
+    for (int i = 0; i < 2; ++i) {
+        int base = i == 0 ? 2 : 3, scale = 1, e = 0;
+        while (scale < std::min(res[i], 128)) { scale *= base; ++e; }
+        scales[i] = scale;
+        exps[i] = e;
+    }
+    uint32_t stride = (uint32_t)(scales[0] * scales[1]);
+    if ((uint64_t)stride * (uint64_t)d->sampler.spp > 0xffffffffull)
+        throw PtError(PT_ERR_UNSUPPORTED, "Halton sample index exceeds 32 bits (spp too large)");
+    s->hpc.exp1 = exps[1];
+    s->hpc.scale0 = (uint32_t)scales[0];
+    s->hpc.mi0 = (uint32_t)mult_inverse(scales[1], scales[0]);
+    s->hpc.mi1 = (uint32_t)mult_inverse(scales[0], scales[1]);
+    int max_dim = std::min(1000, 6 + 8 * (d->integrator.max_depth + 1));
+    std::vector<DivMagic> divs((size_t)max_dim);
+    std::vector<float> c0((size_t)max_dim);
+    for (int i = 0; i < max_dim; ++i) {
+        divs[i] = make_div_magic((uint32_t)ht.primes[i]);
+        const float invBase = (float)1 / (float)ht.primes[i];
+        c0[i] = invBase * (float)ht.perms[(size_t)ht.prime_sums[i]] / (1 - invBase);
+    }
+    size_t nperm = (size_t)(max_dim < 1000 ? ht.prime_sums[max_dim] : (int)ht.perms.size());
+    s->perm.upload(ht.perms.data(), nperm);
+    s->psums.upload(ht.prime_sums.data(), (size_t)max_dim);
+    s->divs.upload(divs);
+    s->perm_c0.upload(c0);
+    s->spp = d->sampler.spp;
+
+    // ---- camera (camera.h ProjectiveCamera, perspective.cpp:45-66) ----
+    const pt_camera_desc& cam = d->camera;
+    HXF camToScreen = hxf_perspective(cam.fov, 1e-2f, 1000.f);
+    const float* sw = cam.screen_window;
+    HXF s2r = hxf_mul(hxf_mul(hxf_scale((float)f.xres, (float)f.yres, 1), hxf_scale(1 / (sw[1] - sw[0]), 1 / (sw[2] - sw[3]), 1)),
+                      hxf_translate(-sw[0], -sw[3], 0));
+    HXF r2c = hxf_mul(hxf_inverse(camToScreen), hxf_inverse(s2r));
+
+    DevScene& ds = s->dev;
+    ds.nodes = s->nodes.p;
+    ds.prims = s->prims.p;
+    ds.n_nodes = (int)s->host_nodes.size();
+    ds.n_prims = (int)s->host_prim_order.size();
+    ds.tris = s->tris.p;
+    ds.P = s->P.p;
+    ds.N = d->N ? s->N.p : nullptr;
+    ds.S = d->S ? s->S.p : nullptr;
+    ds.UV = d->UV ? s->UV.p : nullptr;
+    ds.planes = s->planes.p;
+    ds.portal_planes = s->pplanes.p;
+    ds.mats = s->mats.p;
+    ds.lights = s->lights.p;
+    ds.n_lights = nl;
+    ds.ldist_func = s->lfunc.p;
+    ds.ldist_cdf = s->lcdf.p;
+    ds.ldist_int = funcInt;
+    ds.tri_area = s->tri_area.p;
+    ds.perm = s->perm.p;
+    ds.prime_sums = s->psums.p;
+    ds.divs = s->divs.p;
+    ds.perm_c0 = s->perm_c0.p;
+    ds.max_dim = max_dim;
+    ds.hal_exp0 = exps[0];
+    ds.hal_scale1 = (uint32_t)scales[1];
+    ds.div_scale1 = make_div_magic((uint32_t)scales[1]);
+    if (scales[1] == 1) { ds.div_scale1.magic = 0; ds.div_scale1.shift = 0; }
+    ds.hal_stride = stride;
+    ds.center = d->sampler.sample_pixel_center;
+    ds.r2c = to_m4(r2c.m);
+    std::memcpy(ds.c2w.m, cam.camera_to_world.m, 64);
+    ds.lens_radius = cam.lens_radius;
+    ds.focal_distance = cam.focal_distance;
+    ds.max_depth = d->integrator.max_depth;
+    ds.rr_threshold = d->integrator.rr_threshold;
+}
+
+// Pixels of tiles t with t % stride == offset, tile order then scan order
+// (integrator.cpp:533-560), restricted to the integrator's pixelBounds.
+static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int2>* pix) {
+    pix->clear();
+    int nt = fr.ntx * fr.nty;
+    for (int t = 0; t < nt; ++t) {
+        if (t % stride != offset) continue;
+        int tx = t % fr.ntx, ty = t / fr.ntx;
+        int x0 = fr.sb_x0 + tx * 16, y0 = fr.sb_y0 + ty * 16;
+        int x1 = std::min(x0 + 16, fr.sb_x1), y1 = std::min(y0 + 16, fr.sb_y1);
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x)
+                if (x >= fr.pb_x0 && x < fr.pb_x1 && y >= fr.pb_y0 && y < fr.pb_y1) pix->push_back(make_int2(x, y));
+    }
+}
+
+__global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
+    c[0] = rays;
+    c[1] = paths;
+    c[2] = 0;
+    c[3] = 0;
+    c[4] = 0;
+    c[5] = 0;
+}
+
+struct RenderResult {
+    DevStats st{};
+    double render_ms = 0, trace_ms = 0;
+    uint64_t launches = 0, samples = 0;
+};
+
+// Render the given tiles into the device accumulation buffer d_accum
+// (float4 per cropped pixel).  Synchronous on `stream` (reads queue sizes
+// back once per bounce).
+static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begin, int s_end, float4* d_accum,
+                                 hipStream_t stream) {
+    if (stride <= 0 || offset < 0 || offset >= stride) throw PtError(PT_ERR_INVALID_ARG, "bad tile partition");
+    if (s_begin < 0 || s_end < s_begin) throw PtError(PT_ERR_INVALID_ARG, "bad sample range");
+    if ((uint64_t)s->dev.hal_stride * (uint64_t)s_end > 0xffffffffull)
+        throw PtError(PT_ERR_UNSUPPORTED, "Halton sample index exceeds 32 bits");
+    const Frame& fr = s->fr;
+    std::vector<int2> pix;
+    tile_pixels(fr, offset, stride, &pix);
+    RenderResult rr;
+    const int npix = (int)pix.size();
+    const int sbw = fr.sb_x1 - fr.sb_x0, sbh = fr.sb_y1 - fr.sb_y0;
+    std::vector<int> pixslot((size_t)sbw * sbh, -1);
+    for (int i = 0; i < npix; ++i) pixslot[(size_t)(pix[i].y - fr.sb_y0) * sbw + (pix[i].x - fr.sb_x0)] = i;
+    if (npix == 0) return rr;
+    DBuf<int2> dpix;
+    dpix.upload(pix);
+    DBuf<int> dslot;
+    dslot.upload(pixslot);
+    const int spp = s_end - s_begin;
+    if (spp == 0) return rr;
+    int S = (int)std::max<size_t>(1, std::min<size_t>((size_t)spp, s->target_slots / (size_t)npix));
+    const size_t nslots = (size_t)npix * (size_t)S;
+    const int maxBlocksTrace = s->num_cus * 16;
+    const int maxBlocksShade = s->num_cus * 8;
+    Work& w = s->work;
+    w.ensure(nslots, (size_t)maxBlocksTrace * kTraceBlock);
+    HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
+    DevPaths ps = w.paths((int)nslots);
+    hipEvent_t ev0, ev1;
+    HIPCHK(hipEventCreate(&ev0));
+    HIPCHK(hipEventCreate(&ev1));
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    auto tev_get = [&](size_t i) {
+        while (tev.size() <= i) {
+            hipEvent_t a, b;
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&b));
+            tev.push_back({a, b});
+        }
+        return tev[i];
+    };
+    double trace_ms = 0;
+    size_t tcount = 0;
+    HIPCHK(hipEventRecord(ev0, stream));
+    uint32_t* counts = w.counts.p;
+    uint32_t host_counts[8];
+    for (int s0 = s_begin; s0 < s_end; s0 += S) {
+        const int ns = std::min(S, s_end - s0);
+        const uint32_t nb = (uint32_t)npix * (uint32_t)ns;
+        ps.n = (int)nslots;
+        hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0, stream,
+                           s->dev, ps, dpix.p, npix, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
+        hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
+        HIPCHK(hipGetLastError());
+        uint32_t *rq_in = w.rq0.p, *rq_out = w.rq1.p, *pq_in = w.pq0.p, *pq_out = w.pq1.p;
+        uint32_t nrays = nb, npaths = nb;
+        int iter = 0;
+        while (npaths > 0) {
+            // counts[0]/[1] hold the input sizes, [2]/[3] the output sizes
+            if (nrays > 0) {
+                auto e = tev_get(tcount++);
+                HIPCHK(hipEventRecord(e.first, stream));
+                hipLaunchKernelGGL(k_trace, dim3(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace))),
+                                   dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in, counts + 0, w.spill.p, w.stats.p);
+                HIPCHK(hipEventRecord(e.second, stream));
+                rr.launches++;
+            }
+            hipLaunchKernelGGL(k_shade, dim3(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade))),
+                               dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out, counts + 2, pq_out,
+                               counts + 3, w.stats.p);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            nrays = host_counts[0];
+            npaths = host_counts[1];
+            hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nrays, npaths);
+            std::swap(rq_in, rq_out);
+            std::swap(pq_in, pq_out);
+            if (++iter > 100000) throw PtError(PT_ERR_STATE, "path loop did not terminate");
+        }
+        const int total = fr.width() * fr.height();
+        hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(total, 256), s->num_cus * 16))), dim3(256), 0,
+                           stream, ps, s->film, dslot.p, npix, ns, d_accum);
+        HIPCHK(hipGetLastError());
+        rr.samples += nb;
+    }
+    HIPCHK(hipEventRecord(ev1, stream));
+    HIPCHK(hipMemcpyAsync(&rr.st, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
+    rr.render_ms = ms;
+    for (size_t i = 0; i < tcount; ++i) {
+        float t = 0;
+        HIPCHK(hipEventElapsedTime(&t, tev[i].first, tev[i].second));
+        trace_ms += t;
+    }
+    rr.trace_ms = trace_ms;
+    for (auto& e : tev) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
+    if (rr.st.dim_overflow) throw PtError(PT_ERR_UNSUPPORTED, "Halton dimension table exhausted");
+    return rr;
+}
+
+// Film::MergeFilmTile + Film::WriteImage (film.cpp:117-130, 169-211) for an
+// accumulation buffer holding the RGB contribution sum and weight sum.
+static void resolve(const pt_scene* s, const float* accum, float* rgb) {
+    const Frame& fr = s->fr;
+    size_t np = (size_t)fr.width() * fr.height();
+    const float scale = s->filmdesc.scale;
+    for (size_t o = 0; o < np; ++o) {
+        const float* c = &accum[4 * o];
+        float xyz[3];
+        xyz[0] = 0.412453f * c[0] + 0.357580f * c[1] + 0.180423f * c[2];
+        xyz[1] = 0.212671f * c[0] + 0.715160f * c[1] + 0.072169f * c[2];
+        xyz[2] = 0.019334f * c[0] + 0.119193f * c[1] + 0.950227f * c[2];
+        float px[3] = {0.f + xyz[0], 0.f + xyz[1], 0.f + xyz[2]};
+        float out[3];
+        out[0] = 3.240479f * px[0] - 1.537150f * px[1] - 0.498535f * px[2];
+        out[1] = -0.969256f * px[0] + 1.875991f * px[1] + 0.041556f * px[2];
+        out[2] = 0.055648f * px[0] - 0.204043f * px[1] + 1.057311f * px[2];
+        float ws = 0.f + c[3];
+        if (ws != 0) {
+            float invWt = (float)1 / ws;
+            for (int k = 0; k < 3; ++k) out[k] = smax(0.f, out[k] * invWt);
+        }
+        float splat[3];
+        splat[0] = 3.240479f * 0.f - 1.537150f * 0.f - 0.498535f * 0.f;
+        splat[1] = -0.969256f * 0.f + 1.875991f * 0.f + 0.041556f * 0.f;
+        splat[2] = 0.055648f * 0.f - 0.204043f * 0.f + 1.057311f * 0.f;
+        for (int k = 0; k < 3; ++k) {
+            out[k] += 1.f * splat[k];
+            out[k] *= scale;
+            rgb[3 * o + k] = out[k];
+        }
+    }
+}
+
+static void fill_stats(const RenderResult& r, pt_stats* st) {
+    if (!st) return;
+    st->camera_rays = r.samples;
+    st->closest_rays = r.st.closest;
+    st->shadow_rays = r.st.shadow;
+    st->node_visits = r.st.nodes;
+    st->prim_tests = r.st.prims;
+    st->samples = r.samples;
+    st->render_ms = r.render_ms;
+    st->trace_ms = r.trace_ms;
+    st->trace_launches = r.launches;
+}
+
+template <class F>
+static pt_status guarded(F&& f) {
+    try {
+        f();
+        return PT_OK;
+    } catch (const PtError& e) {
+        g_last_error = e.what();
+        return e.status;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of host memory";
+        return PT_ERR_OOM;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return PT_ERR_STATE;
+    }
+}
+
+static void require_device() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) throw PtError(PT_ERR_DEVICE, "no HIP device available (the product has no CPU fallback)");
+}
+
+}  // namespace pt
+
+using namespace pt;
+
+extern "C" {
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+const char* pt_last_error(void) { return g_last_error.c_str(); }
+
+pt_status pt_load_pbrt(const char* path, pt_host_scene** out) {
+    return guarded([&] {
+        if (!path || !out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        *out = (pt_host_scene*)load_pbrt_file(path);
+    });
+}
+const pt_scene_desc* pt_host_scene_desc(const pt_host_scene* hs) {
+    return hs ? host_scene_desc((const pt_host_scene_impl*)hs) : nullptr;
+}
+void pt_host_scene_free(pt_host_scene* hs) {
+    if (hs) host_scene_free((pt_host_scene_impl*)hs);
+}
+
+pt_status pt_init(int device) {
+    return guarded([&] {
+        require_device();
+        HIPCHK(hipSetDevice(device));
+    });
+}
+
+pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
+    return guarded([&] {
+        if (!out) throw PtError(PT_ERR_INVALID_ARG, "null out");
+        require_device();
+        std::unique_ptr<pt_scene> s(new pt_scene);
+        HIPCHK(hipGetDevice(&s->device));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, s->device));
+        s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        build_scene(s.get(), desc);
+        *out = s.release();
+    });
+}
+
+void pt_scene_destroy(pt_scene* scene) { delete scene; }
+
+pt_status pt_scene_bvh(const pt_scene* s, int32_t* n_nodes, void* nodes32, int32_t* n_prims, int32_t* prim_order) {
+    return guarded([&] {
+        if (!s) throw PtError(PT_ERR_INVALID_ARG, "null scene");
+        if (n_nodes) *n_nodes = (int32_t)s->host_nodes.size();
+        if (n_prims) *n_prims = (int32_t)s->host_prim_order.size();
+        if (nodes32) std::memcpy(nodes32, s->host_nodes.data(), s->host_nodes.size() * sizeof(LinearNode));
+        if (prim_order)
+            for (size_t i = 0; i < s->host_prim_order.size(); ++i) prim_order[i] = s->host_prim_order[i];
+    });
+}
+
+pt_status pt_build_bvh_host(const pt_scene_desc* d, int32_t* n_nodes, void* nodes32, int32_t* prim_order,
+                            int32_t cap) {
+    return guarded([&] {
+        if (!d || !n_nodes) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        std::vector<LinearNode> nodes;
+        std::vector<int> order;
+        build_bvh(d, &nodes, &order);
+        *n_nodes = (int32_t)nodes.size();
+        if (nodes32 && (int32_t)nodes.size() <= cap) std::memcpy(nodes32, nodes.data(), nodes.size() * sizeof(LinearNode));
+        if (prim_order && (int32_t)order.size() <= cap)
+            for (size_t i = 0; i < order.size(); ++i) prim_order[i] = order[i];
+    });
+}
+
+pt_status pt_film_size(const pt_scene* s, int32_t* w, int32_t* h) {
+    return guarded([&] {
+        if (!s) throw PtError(PT_ERR_INVALID_ARG, "null scene");
+        if (w) *w = s->fr.width();
+        if (h) *h = s->fr.height();
+    });
+}
+
+pt_status pt_render_tiles(pt_scene* s, int tile_offset, int tile_stride, float* d_accum, void* stream,
+                          pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !d_accum) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        RenderResult r = render_tiles(s, tile_offset, tile_stride, 0, s->spp, (float4*)d_accum, (hipStream_t)stream);
+        fill_stats(r, stats);
+    });
+}
+
+pt_status pt_render_range(pt_scene* s, int tile_offset, int tile_stride, int sample_begin, int sample_end,
+                          float* d_accum, void* stream, pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !d_accum) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        RenderResult r = render_tiles(s, tile_offset, tile_stride, sample_begin, sample_end, (float4*)d_accum,
+                                      (hipStream_t)stream);
+        fill_stats(r, stats);
+    });
+}
+
+pt_status pt_render_accum(pt_scene* s, int tile_offset, int tile_stride, float* accum_out, pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !accum_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        size_t np = (size_t)s->fr.width() * s->fr.height();
+        DBuf<float4> acc;
+        acc.alloc(np);
+        HIPCHK(hipMemset(acc.p, 0, np * sizeof(float4)));
+        RenderResult r = render_tiles(s, tile_offset, tile_stride, 0, s->spp, acc.p, nullptr);
+        HIPCHK(hipMemcpy(accum_out, acc.p, np * sizeof(float4), hipMemcpyDeviceToHost));
+        fill_stats(r, stats);
+    });
+}
+
+pt_status pt_resolve_film(const pt_scene* s, const float* accum, float* rgb_out) {
+    return guarded([&] {
+        if (!s || !accum || !rgb_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        resolve(s, accum, rgb_out);
+    });
+}
+
+pt_status pt_render(pt_scene* s, float* rgb_out, pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !rgb_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        size_t np = (size_t)s->fr.width() * s->fr.height();
+        DBuf<float4> acc;
+        acc.alloc(np);
+        HIPCHK(hipMemset(acc.p, 0, np * sizeof(float4)));
+        RenderResult r = render_tiles(s, 0, 1, 0, s->spp, acc.p, nullptr);
+        std::vector<float> h(4 * np);
+        HIPCHK(hipMemcpy(h.data(), acc.p, np * sizeof(float4), hipMemcpyDeviceToHost));
+        resolve(s, h.data(), rgb_out);
+        fill_stats(r, stats);
+    });
+}
+
+pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
+    return guarded([&] {
+        if (!s || slots <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        s->target_slots = (size_t)slots;
+    });
+}
+
+pt_status pt_write_pfm(const char* path, const float* rgb, int32_t width, int32_t height) {
+    return guarded([&] {
+        if (!path || !rgb || width <= 0 || height <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        FILE* f = std::fopen(path, "wb");
+        if (!f) throw PtError(PT_ERR_IO, std::string("cannot open ") + path);
+        std::fprintf(f, "PF\n%d %d\n-1\n", width, height);  // little endian (imageio.cpp WritePFM)
+        for (int y = height - 1; y >= 0; --y)
+            std::fwrite(rgb + (size_t)3 * width * y, sizeof(float), (size_t)3 * width, f);
+        std::fclose(f);
+    });
+}
+
+// ---- test hooks ----
+pt_status pt_debug_libm_trig(int n, const float* x, float* sin_out, float* cos_out) {
+    return guarded([&] {
+        for (int i = 0; i < n; ++i) {
+            sin_out[i] = libm_sinf(x[i]);
+            cos_out[i] = libm_cosf(x[i]);
+        }
+    });
+}
+pt_status pt_debug_halton(pt_scene* s, int n, const uint32_t* idx, const int32_t* dims, float* out) {
+    return guarded([&] {
+        DBuf<uint32_t> di; DBuf<int> dd; DBuf<float> o;
+        di.upload(idx, (size_t)n); dd.upload(dims, (size_t)n); o.alloc((size_t)n);
+        hipLaunchKernelGGL(k_debug_halton, dim3(ceil_div(n, 256)), dim3(256), 0, 0, s->dev, di.p, dd.p, n, o.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpy(out, o.p, sizeof(float) * n, hipMemcpyDeviceToHost));
+    });
+}
+pt_status pt_debug_pixel_offsets(pt_scene* s, int n, const int32_t* pixxy, uint32_t* out) {
+    return guarded([&] {
+        DBuf<int2> dp; DBuf<uint32_t> o;
+        dp.upload((const int2*)pixxy, (size_t)n); o.alloc((size_t)n);
+        hipLaunchKernelGGL(k_debug_pixel_offset, dim3(ceil_div(n, 256)), dim3(256), 0, 0, s->dev, s->hpc, dp.p, n, o.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpy(out, o.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    });
+}
+pt_status pt_debug_camera_rays(pt_scene* s, int n, const float* film_xy, float* out6) {
+    return guarded([&] {
+        DBuf<float> df, o;
+        df.upload(film_xy, (size_t)2 * n); o.alloc((size_t)6 * n);
+        hipLaunchKernelGGL(k_debug_camera, dim3(ceil_div(n, 256)), dim3(256), 0, 0, s->dev, df.p, n, o.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpy(out6, o.p, sizeof(float) * 6 * n, hipMemcpyDeviceToHost));
+    });
+}
+pt_status pt_debug_trace(pt_scene* s, int n, const float* rays7, int any, int32_t* out_prim) {
+    return guarded([&] {
+        DBuf<float> dr; DBuf<int> o, sp;
+        dr.upload(rays7, (size_t)7 * n); o.alloc((size_t)n); sp.alloc((size_t)n * (64 - kStackLds));
+        hipLaunchKernelGGL(k_debug_trace, dim3(ceil_div(n, kTraceBlock)), dim3(kTraceBlock), 0, 0, s->dev, dr.p, n,
+                           any, sp.p, o.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpy(out_prim, o.p, sizeof(int) * n, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

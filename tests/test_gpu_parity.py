@@ -1,0 +1,151 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on
+the same inputs.  Integer / index results must be bit-exact; radiance must
+match within the north_star tolerance (per-pixel RMSE < 1e-4 of the image,
+relative to its mean for the unbounded 'projection' estimator)."""
+import numpy as np
+import pytest
+
+import ptgpu
+import pyoracle
+from conftest import furnace_scene
+
+pytestmark = pytest.mark.gpu
+
+MINI = dict(res=(64, 36), spp=16)
+
+
+def _scene(path, **kw):
+    hs = ptgpu.HostScene(path)
+    return hs, ptgpu.Scene(hs, **kw)
+
+
+def _sample_bounds(hs):
+    # box filter r = 0.5: sample bounds == crop window
+    w, h = pyoracle.film_size(hs.desc)
+    return (0, 0, w, h)
+
+
+def test_halton_bit_exact(variant):
+    hs, sc = _scene(variant(**MINI))
+    sb = _sample_bounds(hs)
+    rng = np.random.default_rng(1)
+    n = 4000
+    px = rng.integers(0, sb[2], n)
+    py = rng.integers(0, sb[3], n)
+    s = rng.integers(0, 16, n)
+    dims = rng.integers(0, 40, n).astype(np.int32)
+    idx = np.array([pyoracle.halton_index(sb, int(a), int(b), int(c)) for a, b, c in zip(px, py, s)], np.uint32)
+    ref = np.array([pyoracle.halton_sample(sb, int(a), int(b), int(c), int(d)) for a, b, c, d in zip(px, py, s, dims)],
+                   np.float32)
+    got = sc.debug_halton(idx, dims)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_halton_division_extremes(variant):
+    """Magic-number division by every per-dimension prime, at large indices."""
+    hs, sc = _scene(variant(**MINI))
+    dims = np.arange(2, 46, dtype=np.int32)
+    vals = np.array([0, 1, 2, 3, 4294967295, 4294967294, 2147483648, 123456789, 31103, 31104 * 255 + 31103],
+                    np.uint64)
+    idx = np.repeat(vals, len(dims)).astype(np.uint32)
+    dd = np.tile(dims, len(vals))
+    got = sc.debug_halton(idx, dd)
+    ref = np.array([pyoracle.scrambled_radical_inverse(int(d), int(i)) for i, d in zip(idx, dd)], np.float32)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_pixel_offsets(variant):
+    hs, sc = _scene(variant(res=(300, 200), spp=4))
+    sb = _sample_bounds(hs)
+    pix = np.array([(x, y) for y in range(0, 200, 7) for x in range(0, 300, 5)], np.int32)
+    got = sc.debug_pixel_offsets(pix)
+    ref = np.array([pyoracle.halton_index(sb, int(x), int(y), 0) for x, y in pix], np.uint32)
+    assert np.array_equal(got, ref)
+
+
+def test_camera_rays_bit_exact(variant):
+    hs, sc = _scene(variant(**MINI))
+    rng = np.random.default_rng(2)
+    film = np.stack([rng.uniform(0, 64, 2000), rng.uniform(0, 36, 2000)], 1).astype(np.float32)
+    got = sc.debug_camera_rays(film)
+    ref = np.array([np.concatenate(pyoracle.camera_ray(hs.desc, float(x), float(y))) for x, y in film], np.float32)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def _random_rays(n, seed, tmax=np.inf):
+    rng = np.random.default_rng(seed)
+    o = np.stack([rng.uniform(1, 555, n), rng.uniform(1, 690, n), rng.uniform(-899, 558, n)], 1)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    t = np.full((n, 1), tmax)
+    return np.concatenate([o, d, t], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_traversal_bit_exact(variant, any_hit):
+    hs, sc = _scene(variant(**MINI))
+    rays = _random_rays(20000, 3, tmax=np.inf if not any_hit else 300.0)
+    _, order = sc.bvh()
+    got = sc.debug_trace(rays, any_hit)
+    ref = pyoracle.trace(hs.desc, rays, any_hit)
+    if not any_hit:
+        got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
+    else:
+        got = (got >= 0).astype(np.int32)
+    assert np.array_equal(got, ref)
+
+
+def test_bvh_device_matches_oracle(variant):
+    hs, sc = _scene(variant(**MINI))
+    n1, o1 = sc.bvh()
+    n2, o2 = pyoracle.build_bvh(hs.desc)
+    assert np.array_equal(n1, n2)
+    assert np.array_equal(o1, o2[:len(o1)])
+
+
+def _rmse(a, b):
+    # imgtool diff metric: MSE over 3*w*h channel values (src/tools/imgtool.cpp:333-441)
+    return float(np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("strategy", ["portal", "light", "projection"])
+def test_render_matches_oracle(variant, strategy):
+    path = variant(strategy=strategy, **MINI)
+    hs, sc = _scene(path)
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    assert got.shape == ref.shape
+    assert np.isfinite(got).all()
+    rmse = _rmse(got, ref)
+    scale = max(1.0, float(np.mean(ref)))
+    exact = float(np.mean(np.all(got.view(np.uint32) == ref.view(np.uint32), axis=2)))
+    print(f"{strategy}: rmse={rmse:.3g} mean={ref.mean():.5g} bit-exact pixels={exact:.4f} "
+          f"rays gpu={gst['closest_rays']}/{gst['shadow_rays']} oracle={rst['closest_rays']}/{rst['shadow_rays']}")
+    assert rmse / scale < 1e-4
+    assert exact > 0.99
+    assert gst["camera_rays"] == rst["camera_rays"]
+    assert abs(gst["closest_rays"] - rst["closest_rays"]) <= 1e-3 * rst["closest_rays"]
+
+
+def test_render_accum_tiles_partition(variant):
+    hs, sc = _scene(variant(**MINI))
+    full, _ = sc.render_accum(0, 1)
+    a0, _ = sc.render_accum(0, 2)
+    a1, _ = sc.render_accum(1, 2)
+    np.testing.assert_allclose(a0 + a1, full, rtol=1e-6, atol=1e-6)
+
+
+def test_furnace_known_answer(tmp_path):
+    """src/tests/analytic_scenes.cpp:135-165 known answer (1.0 +- 0.02)."""
+    hs, sc = _scene(furnace_scene(tmp_path, res=10, spp=256, maxdepth=8))
+    img, _ = sc.render()
+    assert abs(float(img.mean()) - 1.0) < 0.02
+
+
+def test_small_batches_equal_large(variant):
+    """Batching the sample range differently must not change the image."""
+    path = variant(**MINI)
+    hs = ptgpu.HostScene(path)
+    a, _ = ptgpu.Scene(hs).render()
+    b, _ = ptgpu.Scene(hs, batch_slots=64 * 36 * 3).render()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
