@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--res", default="", help="override WxH")
     ap.add_argument("--strategy", default="", help="override portal strategy")
     ap.add_argument("--batch-slots", type=int, default=0)
+    ap.add_argument("--shard", default="samples", help="samples (weak) | samples-split | tiles (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -94,6 +95,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import ptgpu
+    import shard as shardmod
 
     tmpdir = os.environ.get("TMPDIR", "/tmp")
     spath = os.path.join(tmpdir, f"bench_scene_{os.getpid()}.pbrt")
@@ -106,14 +108,11 @@ def main():
     spp = int(re.search(r'"integer pixelsamples" \[(\d+)\]', open(spath).read()).group(1))
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
-    s_begin, s_end = rank * spp, (rank + 1) * spp
+    my = shardmod.plan(rank, world, spp, args.shard)
+    render = shardmod.device_renderer(sc, accum.data_ptr(), stream)
 
     def step():
-        accum.zero_()
-        st = sc.render_range_device(0, 1, s_begin, s_end, accum.data_ptr(), stream)
-        if world > 1:
-            dist.reduce(accum, dst=0)
-        return st
+        return shardmod.render_frame(my, render, accum, shardmod.reduce_to_root)
 
     for _ in range(args.warmup):
         step()
@@ -156,13 +155,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.shard == "samples" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)",
-            "config": {"workload": f"portal Cornell (config 2) {w}x{h} @{spp}spp/rank, path maxdepth 5, "
-                                   f"sample-range sharded", "resolution": [w, h], "spp_per_rank": spp,
-                       "parallelism": f"sample-range x{world}"},
+            "config": {"workload": f"portal Cornell (config 2) {w}x{h} @{spp}spp"
+                                   f"{'/rank' if args.shard == 'samples' else ''}, path maxdepth 5, "
+                                   f"{args.shard}-sharded", "resolution": [w, h],
+                       "frame_spp": shardmod.frame_samples(spp, world, args.shard),
+                       "parallelism": f"{args.shard} x{world}"},
             "mrays_per_s": round(total_rays / dt / 1e6, 2),
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -248,9 +248,12 @@ pt_status pt_render(pt_scene* scene, float* rgb_out, pt_stats* stats);
 
 /* Multi-GPU building block: render the 16x16 image tiles t with
  * t % tile_stride == tile_offset into a device-resident accumulation buffer
- * (4 floats per cropped pixel: RGB contribution sum + filter weight sum,
- * zeroed by the caller), on `stream` (hipStream_t, may be NULL).  Returns
- * when the work is enqueued; the caller synchronises. */
+ * (4 floats per cropped pixel: Film::Pixel's xyz[3] + filterWeightSum
+ * (film.h:98-105), zeroed by the caller), on `stream` (hipStream_t, may be
+ * NULL).  Each tile's FilmTile partial sum is formed in the reference's
+ * order and merged in tile order (film.cpp:117-130), so buffers from
+ * disjoint tile sets or sample ranges combine by plain addition.  Returns
+ * when the work is done (the call synchronises `stream`). */
 pt_status pt_render_tiles(pt_scene* scene, int tile_offset, int tile_stride,
                           float* d_accum, void* stream, pt_stats* stats);
 
@@ -261,9 +264,16 @@ pt_status pt_render_range(pt_scene* scene, int tile_offset, int tile_stride,
                           int sample_begin, int sample_end, float* d_accum,
                           void* stream, pt_stats* stats);
 
-/* Resolve an accumulation buffer (host memory, 4 floats per pixel) into the
- * final RGB image exactly as Film::MergeFilmTile + Film::WriteImage do. */
+/* Resolve an accumulation buffer (host memory, 4 floats per pixel: XYZ sum +
+ * weight sum) into the final RGB image exactly as Film::WriteImage does
+ * (film.cpp:169-211). */
 pt_status pt_resolve_film(const pt_scene* scene, const float* accum, float* rgb_out);
+
+/* Host-only variants (no device needed): resolve an accumulation buffer
+ * with the film parameters of a scene description, and its cropped size.
+ * Used by rank 0 after the cross-rank reduce and by CPU tests. */
+pt_status pt_resolve_film_host(const pt_scene_desc* desc, const float* accum, float* rgb_out);
+pt_status pt_film_size_host(const pt_scene_desc* desc, int32_t* width, int32_t* height);
 
 /* Same as pt_render_tiles but synchronous, into a host buffer (4 floats per
  * cropped pixel, zero-initialised by the call). */

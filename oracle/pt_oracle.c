@@ -388,6 +388,7 @@ typedef struct {
     /* halton */
     int base_scales[2], base_exps[2], sample_stride, mult_inverse[2];
     int spp;
+    int s_begin, s_end;  /* camera-sample index range rendered per pixel */
     int max_depth;
     float rr_threshold;
     int pix_x0, pix_y0, pix_x1, pix_y1; /* integrator pixelBounds */
@@ -1587,7 +1588,7 @@ static void render_tile(const Scene* sc, const Halton* h, int tx, int ty, FilmTi
         for (int x = x0; x < x1; ++x) {
             if (!(x >= sc->pix_x0 && x < sc->pix_x1 && y >= sc->pix_y0 && y < sc->pix_y1)) continue;
             int64_t off = halton_pixel_offset(h, x, y);
-            for (int s = 0; s < sc->spp; ++s) {
+            for (int s = sc->s_begin; s < sc->s_end; ++s) {
                 Samp smp = {h, off + (int64_t)s * h->stride, 0};
                 float uf[2], ul[2];
                 get2d(&smp, uf);                 /* pFilm */
@@ -1665,6 +1666,8 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     camera_init(sc);
     film_init(sc);
     sc->spp = d->sampler.spp;
+    sc->s_begin = 0;
+    sc->s_end = d->sampler.spp;
     sc->max_depth = d->integrator.max_depth;
     sc->rr_threshold = d->integrator.rr_threshold;
     sc->pix_x0 = sc->sb_x0; sc->pix_y0 = sc->sb_y0; sc->pix_x1 = sc->sb_x1; sc->pix_y1 = sc->sb_y1;
@@ -1715,14 +1718,15 @@ static void* worker(void* arg) {
     return NULL;
 }
 
-/* Renders tiles; returns the per-pixel film XYZ + weight after
- * Film::MergeFilmTile in tile order (film.cpp:117-130), and optionally the RGB
- * contribution accumulation. */
+/* Renders tiles; forms the per-pixel film XYZ + weight by Film::MergeFilmTile
+ * in tile order (film.cpp:117-130), optionally returned as accum_out, and
+ * optionally the resolved RGB image. */
 static int render_common(const pt_scene_desc* desc, float* rgb_out, float* accum_out, int nthreads, int max_tiles,
-                         int tile_offset, int tile_stride, oracle_stats* stats) {
+                         int tile_offset, int tile_stride, int s_begin, int s_end, oracle_stats* stats) {
     Scene sc;
     if (!desc) return 1;
     scene_setup(&sc, desc);
+    if (s_end >= 0) { sc.s_begin = s_begin; sc.s_end = s_end; }
     Halton h;
     halton_init(&h, sc.sb_x0, sc.sb_y0, sc.sb_x1, sc.sb_y1, desc->sampler.sample_pixel_center);
     int ex = sc.sb_x1 - sc.sb_x0, ey = sc.sb_y1 - sc.sb_y0;
@@ -1759,7 +1763,7 @@ static int render_common(const pt_scene_desc* desc, float* rgb_out, float* accum
                 for (int i = 0; i < 3; ++i) xyz[4 * o + i] += x3[i];
                 xyz[4 * o + 3] += tp->w;
                 if (accum_out) {
-                    for (int i = 0; i < 3; ++i) accum_out[4 * o + i] += tp->c[i];
+                    for (int i = 0; i < 3; ++i) accum_out[4 * o + i] += x3[i];
                     accum_out[4 * o + 3] += tp->w;
                 }
             }
@@ -1800,11 +1804,15 @@ static int render_common(const pt_scene_desc* desc, float* rgb_out, float* accum
 }
 
 int oracle_render(const pt_scene_desc* desc, float* rgb_out, int nthreads, int max_tiles, oracle_stats* stats) {
-    return render_common(desc, rgb_out, NULL, nthreads, max_tiles, 0, 1, stats);
+    return render_common(desc, rgb_out, NULL, nthreads, max_tiles, 0, 1, 0, -1, stats);
 }
 int oracle_render_accum(const pt_scene_desc* desc, float* accum_out, int nthreads, int tile_offset, int tile_stride,
                         oracle_stats* stats) {
-    return render_common(desc, NULL, accum_out, nthreads, -1, tile_offset, tile_stride, stats);
+    return render_common(desc, NULL, accum_out, nthreads, -1, tile_offset, tile_stride, 0, -1, stats);
+}
+int oracle_render_range(const pt_scene_desc* desc, float* accum_out, int nthreads, int tile_offset, int tile_stride,
+                        int s_begin, int s_end, oracle_stats* stats) {
+    return render_common(desc, NULL, accum_out, nthreads, -1, tile_offset, tile_stride, s_begin, s_end, stats);
 }
 void oracle_set_trig(int correctly_rounded) { g_cr_trig = correctly_rounded; }
 int oracle_film_size(const pt_scene_desc* desc, int* w, int* h) {

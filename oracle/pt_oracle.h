@@ -44,11 +44,18 @@ typedef struct oracle_stats {
 int oracle_render(const pt_scene_desc* desc, float* rgb_out, int nthreads,
                   int max_tiles, oracle_stats* stats);
 
-/* Like oracle_render, but returns the un-resolved accumulation buffer
- * (4 floats per cropped pixel: RGB contribution sum, filter weight sum) --
- * the quantity the GPU film accumulates, before XYZ conversion. */
+/* Like oracle_render, but returns the un-resolved film (4 floats per cropped
+ * pixel: Film::Pixel xyz[3] + filterWeightSum after merging the selected
+ * tiles in tile order) -- the quantity the GPU film accumulates. */
 int oracle_render_accum(const pt_scene_desc* desc, float* accum_out,
                         int nthreads, int tile_offset, int tile_stride,
+                        oracle_stats* stats);
+
+/* Accumulation for camera-sample indices [s_begin, s_end) of every pixel of
+ * tiles t % tile_stride == tile_offset (the Halton sequence continues past
+ * the scene's spp). */
+int oracle_render_range(const pt_scene_desc* desc, float* accum_out, int nthreads,
+                        int tile_offset, int tile_stride, int s_begin, int s_end,
                         oracle_stats* stats);
 
 /* 0: libm cosf/sinf as the reference binary calls them (default);

@@ -44,6 +44,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_render.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(oracle_stats)]
         L.oracle_render_accum.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(oracle_stats)]
+        L.oracle_render_range.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(oracle_stats)]
         L.oracle_set_trig.argtypes = [ctypes.c_int]
         L.oracle_set_trig.restype = None
         L.oracle_film_size.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -92,6 +94,16 @@ def render_accum(desc: int, nthreads: int = 1, tile_offset: int = 0, tile_stride
     st = oracle_stats()
     lib().oracle_render_accum(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride,
                               ctypes.byref(st))
+    return acc, st.as_dict()
+
+
+def render_range(desc: int, s_begin: int, s_end: int, nthreads: int = 1, tile_offset: int = 0,
+                 tile_stride: int = 1) -> Tuple[np.ndarray, dict]:
+    w, h = film_size(desc)
+    acc = np.zeros((h, w, 4), np.float32)
+    st = oracle_stats()
+    lib().oracle_render_range(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride, s_begin,
+                              s_end, ctypes.byref(st))
     return acc, st.as_dict()
 
 

@@ -595,50 +595,75 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps,
 }
 
 // ----------------------------------------------------------------------------
-// Film: gather the batch's samples into each pixel in sample order
-// (FilmTile::AddSample film.h:121-161 + the radiance sanitiser,
-// integrator.cpp:592-613).  Accumulates RGB contribution sums + weights.
+// Film: for every film pixel of the batch's region, rebuild each FilmTile's
+// partial sum in the reference's order -- the tile's pixels in scan order,
+// each pixel's samples in order (SamplerIntegrator::Render,
+// integrator.cpp:533-560; FilmTile::AddSample film.h:121-161 + the radiance
+// sanitiser integrator.cpp:592-613) -- then merge the partials tile by tile
+// in tile order as XYZ (Film::MergeFilmTile film.cpp:117-130).  A pure
+// gather: deterministic, no float atomics.  Bit-identical to the reference
+// whenever a batch holds all samples of its tiles.
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int npix,
-                                              int nsamp, float4* accum) {
-    const int cw = fc.crop_x1 - fc.crop_x0, ch = fc.crop_y1 - fc.crop_y0;
-    const int total = cw * ch;
+__global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
+                                              int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum) {
     const uint32_t N = (uint32_t)ps.n;
+    const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
+    const int total = bw * bh;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        const int tx = fc.crop_x0 + t % cw, ty = fc.crop_y0 + t / cw;
-        float4 acc = accum[t];
+        const int tx = bx0 + t % bw, ty = by0 + t / bw;
+        const int wy0 = max(ty - fc.win, fc.sb_y0), wy1 = min(ty + fc.win, fc.sb_y1 - 1);
+        const int wx0 = max(tx - fc.win, fc.sb_x0), wx1 = min(tx + fc.win, fc.sb_x1 - 1);
+        if (wy0 > wy1 || wx0 > wx1) continue;
+        const size_t o = (size_t)(ty - fc.crop_y0) * cw + (tx - fc.crop_x0);
+        float4 acc = accum[o];
         bool touched = false;
-        for (int sl = 0; sl < nsamp; ++sl) {
-            for (int qy = ty - fc.win; qy <= ty + fc.win; ++qy) {
-                if (qy < fc.sb_y0 || qy >= fc.sb_y1) continue;
-                for (int qx = tx - fc.win; qx <= tx + fc.win; ++qx) {
-                    if (qx < fc.sb_x0 || qx >= fc.sb_x1) continue;
-                    const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)];
-                    if (p < 0) continue;
-                    const uint32_t slot = (uint32_t)sl * (uint32_t)npix + (uint32_t)p;
-                    const float2 pf = ps.pfilm[slot];
-                    const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
-                    const int x0 = (int)ceilf(dx - fc.rx), x1 = (int)floorf(dx + fc.rx) + 1;
-                    const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
-                    if (tx < x0 || tx >= x1 || ty < y0 || ty >= y1) continue;
-                    S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
-                    if (has_nan(L)) L = s3(0.f);
-                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
-                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
-                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
-                    const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
-                    const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
-                    int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
-                    int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
-                    const float w = fc.table[iy * 16 + ix];
-                    const S3 c = (L * 1.f) * w;
-                    acc.x += c.c[0]; acc.y += c.c[1]; acc.z += c.c[2]; acc.w += w;
-                    touched = true;
+        const int ty0 = (wy0 - fc.sb_y0) >> 4, ty1 = (wy1 - fc.sb_y0) >> 4;
+        const int tx0 = (wx0 - fc.sb_x0) >> 4, tx1 = (wx1 - fc.sb_x0) >> 4;
+        for (int tr = ty0; tr <= ty1; ++tr) {
+            for (int tc = tx0; tc <= tx1; ++tc) {
+                const int qy0 = max(wy0, fc.sb_y0 + 16 * tr), qy1 = min(wy1, fc.sb_y0 + 16 * tr + 15);
+                const int qx0 = max(wx0, fc.sb_x0 + 16 * tc), qx1 = min(wx1, fc.sb_x0 + 16 * tc + 15);
+                S3 part = s3(0.f);
+                float wsum = 0.f;
+                bool any = false;
+                for (int qy = qy0; qy <= qy1; ++qy) {
+                    for (int qx = qx0; qx <= qx1; ++qx) {
+                        const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
+                        if (p < 0 || p >= np) continue;
+                        for (int sl = 0; sl < nsamp; ++sl) {
+                            const uint32_t slot = (uint32_t)sl * (uint32_t)np + (uint32_t)p;
+                            const float2 pf = ps.pfilm[slot];
+                            const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
+                            const int x0 = (int)ceilf(dx - fc.rx), x1 = (int)floorf(dx + fc.rx) + 1;
+                            const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
+                            if (tx < x0 || tx >= x1 || ty < y0 || ty >= y1) continue;
+                            S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                            if (has_nan(L)) L = s3(0.f);
+                            else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
+                            else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
+                            if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                            const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
+                            const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
+                            int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                            int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                            const float w = fc.table[iy * 16 + ix];
+                            part = part + (L * 1.f) * w;
+                            wsum += w;
+                            any = true;
+                        }
+                    }
                 }
+                if (!any) continue;
+                // RGBSpectrum::ToXYZ (spectrum.h:64-68) of the tile pixel, merged
+                acc.x += 0.412453f * part.c[0] + 0.357580f * part.c[1] + 0.180423f * part.c[2];
+                acc.y += 0.212671f * part.c[0] + 0.715160f * part.c[1] + 0.072169f * part.c[2];
+                acc.z += 0.019334f * part.c[0] + 0.119193f * part.c[1] + 0.950227f * part.c[2];
+                acc.w += wsum;
+                touched = true;
             }
         }
-        if (touched) accum[t] = acc;
+        if (touched) accum[o] = acc;
     }
 }
 

@@ -5,6 +5,7 @@
 // independent paths through camera -> {trace, shade}* -> film kernels.
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -518,17 +519,26 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
 
 // Pixels of tiles t with t % stride == offset, tile order then scan order
 // (integrator.cpp:533-560), restricted to the integrator's pixelBounds.
-static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int2>* pix) {
+// tiles receives, per selected non-empty tile, its first index into pix and
+// its pixel rectangle.
+struct TileSpan {
+    int first;
+    int x0, y0, x1, y1;
+};
+static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int2>* pix, std::vector<TileSpan>* tiles) {
     pix->clear();
+    tiles->clear();
     int nt = fr.ntx * fr.nty;
     for (int t = 0; t < nt; ++t) {
         if (t % stride != offset) continue;
         int tx = t % fr.ntx, ty = t / fr.ntx;
         int x0 = fr.sb_x0 + tx * 16, y0 = fr.sb_y0 + ty * 16;
         int x1 = std::min(x0 + 16, fr.sb_x1), y1 = std::min(y0 + 16, fr.sb_y1);
+        const int first = (int)pix->size();
         for (int y = y0; y < y1; ++y)
             for (int x = x0; x < x1; ++x)
                 if (x >= fr.pb_x0 && x < fr.pb_x1 && y >= fr.pb_y0 && y < fr.pb_y1) pix->push_back(make_int2(x, y));
+        if ((int)pix->size() > first) tiles->push_back({first, x0, y0, x1, y1});
     }
 }
 
@@ -558,27 +568,62 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         throw PtError(PT_ERR_UNSUPPORTED, "Halton sample index exceeds 32 bits");
     const Frame& fr = s->fr;
     std::vector<int2> pix;
-    tile_pixels(fr, offset, stride, &pix);
+    std::vector<TileSpan> tiles;
+    tile_pixels(fr, offset, stride, &pix, &tiles);
     RenderResult rr;
     const int npix = (int)pix.size();
+    const int spp = s_end - s_begin;
+    if (npix == 0 || spp == 0) return rr;
     const int sbw = fr.sb_x1 - fr.sb_x0, sbh = fr.sb_y1 - fr.sb_y0;
     std::vector<int> pixslot((size_t)sbw * sbh, -1);
     for (int i = 0; i < npix; ++i) pixslot[(size_t)(pix[i].y - fr.sb_y0) * sbw + (pix[i].x - fr.sb_x0)] = i;
-    if (npix == 0) return rr;
+    // Batches are groups of whole tiles (in tile order) x runs of samples:
+    // as many tiles as fit target_slots with all their samples, so each
+    // batch carries complete FilmTiles; a single tile too large for that
+    // runs its samples in chunks of S.
+    struct Group {
+        int p0, np, S;
+        int bx0, by0, bx1, by1;
+    };
+    std::vector<Group> groups;
+    const size_t target = std::max<size_t>(1, s->target_slots);
+    size_t max_slots = 0;
+    for (size_t i = 0; i < tiles.size();) {
+        size_t j = i;
+        size_t gp = 0;
+        Group g{tiles[i].first, 0, 0, INT_MAX, INT_MAX, INT_MIN, INT_MIN};
+        while (j < tiles.size()) {
+            const size_t tp = (size_t)((j + 1 < tiles.size() ? tiles[j + 1].first : npix) - tiles[j].first);
+            if (j > i && (gp + tp) * (size_t)spp > target) break;
+            gp += tp;
+            g.bx0 = std::min(g.bx0, tiles[j].x0);
+            g.by0 = std::min(g.by0, tiles[j].y0);
+            g.bx1 = std::max(g.bx1, tiles[j].x1);
+            g.by1 = std::max(g.by1, tiles[j].y1);
+            ++j;
+        }
+        g.np = (int)gp;
+        g.S = (int)std::max<size_t>(1, std::min<size_t>((size_t)spp, target / gp));
+        // film pixels the group's samples can reach: its rectangle grown by
+        // the filter window, clipped to the cropped film
+        g.bx0 = std::max(g.bx0 - s->film.win, s->film.crop_x0);
+        g.by0 = std::max(g.by0 - s->film.win, s->film.crop_y0);
+        g.bx1 = std::min(g.bx1 + s->film.win, s->film.crop_x1);
+        g.by1 = std::min(g.by1 + s->film.win, s->film.crop_y1);
+        max_slots = std::max(max_slots, gp * (size_t)g.S);
+        groups.push_back(g);
+        i = j;
+    }
     DBuf<int2> dpix;
     dpix.upload(pix);
     DBuf<int> dslot;
     dslot.upload(pixslot);
-    const int spp = s_end - s_begin;
-    if (spp == 0) return rr;
-    int S = (int)std::max<size_t>(1, std::min<size_t>((size_t)spp, s->target_slots / (size_t)npix));
-    const size_t nslots = (size_t)npix * (size_t)S;
     const int maxBlocksTrace = s->num_cus * 16;
     const int maxBlocksShade = s->num_cus * 8;
     Work& w = s->work;
-    w.ensure(nslots, (size_t)maxBlocksTrace * kTraceBlock);
+    w.ensure(max_slots, (size_t)maxBlocksTrace * kTraceBlock);
     HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
-    DevPaths ps = w.paths((int)nslots);
+    DevPaths ps = w.paths((int)max_slots);
     hipEvent_t ev0, ev1;
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
@@ -597,45 +642,51 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     HIPCHK(hipEventRecord(ev0, stream));
     uint32_t* counts = w.counts.p;
     uint32_t host_counts[8];
-    for (int s0 = s_begin; s0 < s_end; s0 += S) {
-        const int ns = std::min(S, s_end - s0);
-        const uint32_t nb = (uint32_t)npix * (uint32_t)ns;
-        ps.n = (int)nslots;
-        hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0, stream,
-                           s->dev, ps, dpix.p, npix, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
-        hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
-        HIPCHK(hipGetLastError());
-        uint32_t *rq_in = w.rq0.p, *rq_out = w.rq1.p, *pq_in = w.pq0.p, *pq_out = w.pq1.p;
-        uint32_t nrays = nb, npaths = nb;
-        int iter = 0;
-        while (npaths > 0) {
-            // counts[0]/[1] hold the input sizes, [2]/[3] the output sizes
-            if (nrays > 0) {
-                auto e = tev_get(tcount++);
-                HIPCHK(hipEventRecord(e.first, stream));
-                hipLaunchKernelGGL(k_trace, dim3(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace))),
-                                   dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in, counts + 0, w.spill.p, w.stats.p);
-                HIPCHK(hipEventRecord(e.second, stream));
-                rr.launches++;
-            }
-            hipLaunchKernelGGL(k_shade, dim3(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade))),
-                               dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out, counts + 2, pq_out,
-                               counts + 3, w.stats.p);
+    for (const Group& g : groups) {
+        for (int s0 = s_begin; s0 < s_end; s0 += g.S) {
+            const int ns = std::min(g.S, s_end - s0);
+            const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
+            hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
+                               stream, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
+            hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipStreamSynchronize(stream));
-            nrays = host_counts[0];
-            npaths = host_counts[1];
-            hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nrays, npaths);
-            std::swap(rq_in, rq_out);
-            std::swap(pq_in, pq_out);
-            if (++iter > 100000) throw PtError(PT_ERR_STATE, "path loop did not terminate");
+            uint32_t *rq_in = w.rq0.p, *rq_out = w.rq1.p, *pq_in = w.pq0.p, *pq_out = w.pq1.p;
+            uint32_t nrays = nb, npaths = nb;
+            int iter = 0;
+            while (npaths > 0) {
+                // counts[0]/[1] hold the input sizes, [2]/[3] the output sizes
+                if (nrays > 0) {
+                    auto e = tev_get(tcount++);
+                    HIPCHK(hipEventRecord(e.first, stream));
+                    hipLaunchKernelGGL(k_trace,
+                                       dim3(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace))),
+                                       dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in, counts + 0, w.spill.p,
+                                       w.stats.p);
+                    HIPCHK(hipEventRecord(e.second, stream));
+                    rr.launches++;
+                }
+                hipLaunchKernelGGL(k_shade, dim3(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade))),
+                                   dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out, counts + 2,
+                                   pq_out, counts + 3, w.stats.p);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                nrays = host_counts[0];
+                npaths = host_counts[1];
+                hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nrays, npaths);
+                std::swap(rq_in, rq_out);
+                std::swap(pq_in, pq_out);
+                if (++iter > 100000) throw PtError(PT_ERR_STATE, "path loop did not terminate");
+            }
+            const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
+            if (bw > 0 && bh > 0) {
+                hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(bw * bh, 256), s->num_cus * 16))),
+                                   dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
+                                   d_accum);
+                HIPCHK(hipGetLastError());
+            }
+            rr.samples += nb;
         }
-        const int total = fr.width() * fr.height();
-        hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(total, 256), s->num_cus * 16))), dim3(256), 0,
-                           stream, ps, s->film, dslot.p, npix, ns, d_accum);
-        HIPCHK(hipGetLastError());
-        rr.samples += nb;
     }
     HIPCHK(hipEventRecord(ev1, stream));
     HIPCHK(hipMemcpyAsync(&rr.st, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost, stream));
@@ -659,19 +710,12 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     return rr;
 }
 
-// Film::MergeFilmTile + Film::WriteImage (film.cpp:117-130, 169-211) for an
-// accumulation buffer holding the RGB contribution sum and weight sum.
-static void resolve(const pt_scene* s, const float* accum, float* rgb) {
-    const Frame& fr = s->fr;
-    size_t np = (size_t)fr.width() * fr.height();
-    const float scale = s->filmdesc.scale;
+// Film::WriteImage (film.cpp:169-211) for an accumulation buffer holding
+// Film::Pixel's XYZ sum and filter weight sum.
+static void resolve_film(size_t np, float scale, const float* accum, float* rgb) {
     for (size_t o = 0; o < np; ++o) {
         const float* c = &accum[4 * o];
-        float xyz[3];
-        xyz[0] = 0.412453f * c[0] + 0.357580f * c[1] + 0.180423f * c[2];
-        xyz[1] = 0.212671f * c[0] + 0.715160f * c[1] + 0.072169f * c[2];
-        xyz[2] = 0.019334f * c[0] + 0.119193f * c[1] + 0.950227f * c[2];
-        float px[3] = {0.f + xyz[0], 0.f + xyz[1], 0.f + xyz[2]};
+        const float px[3] = {c[0], c[1], c[2]};
         float out[3];
         out[0] = 3.240479f * px[0] - 1.537150f * px[1] - 0.498535f * px[2];
         out[1] = -0.969256f * px[0] + 1.875991f * px[1] + 0.041556f * px[2];
@@ -691,6 +735,20 @@ static void resolve(const pt_scene* s, const float* accum, float* rgb) {
             rgb[3 * o + k] = out[k];
         }
     }
+}
+
+static void resolve(const pt_scene* s, const float* accum, float* rgb) {
+    resolve_film((size_t)s->fr.width() * s->fr.height(), s->filmdesc.scale, accum, rgb);
+}
+
+// Cropped film size from the description alone (Film::Film, film.cpp:50-60).
+static void crop_size(const pt_film_desc& f, int* w, int* h) {
+    if (f.xres <= 0 || f.yres <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad film resolution");
+    const int x0 = (int)std::ceil((float)f.xres * f.crop[0]), x1 = (int)std::ceil((float)f.xres * f.crop[1]);
+    const int y0 = (int)std::ceil((float)f.yres * f.crop[2]), y1 = (int)std::ceil((float)f.yres * f.crop[3]);
+    if (x1 <= x0 || y1 <= y0) throw PtError(PT_ERR_INVALID_ARG, "empty crop window");
+    *w = x1 - x0;
+    *h = y1 - y0;
 }
 
 static void fill_stats(const RenderResult& r, pt_stats* st) {
@@ -843,6 +901,25 @@ pt_status pt_resolve_film(const pt_scene* s, const float* accum, float* rgb_out)
     return guarded([&] {
         if (!s || !accum || !rgb_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
         resolve(s, accum, rgb_out);
+    });
+}
+
+pt_status pt_resolve_film_host(const pt_scene_desc* d, const float* accum, float* rgb_out) {
+    return guarded([&] {
+        if (!d || !accum || !rgb_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        int w = 0, h = 0;
+        crop_size(d->film, &w, &h);
+        resolve_film((size_t)w * h, d->film.scale, accum, rgb_out);
+    });
+}
+
+pt_status pt_film_size_host(const pt_scene_desc* d, int32_t* w, int32_t* h) {
+    return guarded([&] {
+        if (!d) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        int ww = 0, hh = 0;
+        crop_size(d->film, &ww, &hh);
+        if (w) *w = ww;
+        if (h) *h = hh;
     });
 }
 

@@ -74,6 +74,8 @@ def lib() -> ctypes.CDLL:
     L.pt_render_range.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
                                   ctypes.POINTER(pt_stats)]
     L.pt_resolve_film.argtypes = [vp, f32p, f32p]
+    L.pt_resolve_film_host.argtypes = [vp, f32p, f32p]
+    L.pt_film_size_host.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_set_batch_slots.argtypes = [vp, ctypes.c_int64]
     L.pt_write_pfm.argtypes = [ctypes.c_char_p, f32p, i32, i32]
     L.pt_debug_libm_trig.argtypes = [ctypes.c_int, vp, vp, vp]
@@ -117,6 +119,22 @@ class HostScene:
         _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), nodes.ctypes.data, order.ctypes.data,
                                        int(2 * n.value)))
         return nodes, order
+
+    def film_size(self) -> Tuple[int, int]:
+        """Cropped film (width, height) -- host only."""
+        w, h = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().pt_film_size_host(self.desc, ctypes.byref(w), ctypes.byref(h)))
+        return w.value, h.value
+
+    def resolve(self, accum: np.ndarray) -> np.ndarray:
+        """Film::WriteImage of an (h, w, 4) XYZ+weight accumulation -- host only."""
+        w, h = self.film_size()
+        accum = np.ascontiguousarray(accum, np.float32)
+        if accum.size != 4 * w * h:
+            raise PtError(1, f"accumulation buffer has {accum.size} floats, film needs {4 * w * h}")
+        rgb = np.zeros((h, w, 3), np.float32)
+        _check(lib().pt_resolve_film_host(self.desc, _fptr(accum), _fptr(rgb)))
+        return rgb
 
     def close(self) -> None:
         if self._h:

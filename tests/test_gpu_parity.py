@@ -149,3 +149,44 @@ def test_small_batches_equal_large(variant):
     a, _ = ptgpu.Scene(hs).render()
     b, _ = ptgpu.Scene(hs, batch_slots=64 * 36 * 3).render()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_film_accumulation_matches_oracle(variant):
+    """The device film (XYZ + weight per pixel, tile partials merged in tile
+    order) against the oracle's Film::MergeFilmTile result."""
+    hs, sc = _scene(variant(**MINI))
+    got, _ = sc.render_accum(0, 1)
+    ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
+    exact = float(np.mean(np.all(got.view(np.uint32) == ref.view(np.uint32), axis=2)))
+    print(f"film: bit-exact pixels={exact:.4f} max|d|={np.abs(got - ref).max():.3g}")
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    assert exact > 0.99
+
+
+def test_sample_range_matches_oracle(variant):
+    """pt_render_range (the bench's sharding unit) for samples [16, 24) --
+    past the scene's spp, as rank 1 of a weak-scaled run renders them."""
+    import torch
+    hs, sc = _scene(variant(**MINI))
+    w, h = sc.film_size()
+    acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    sc.render_range_device(0, 1, 16, 24, acc.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = acc.cpu().numpy()
+    ref, _ = pyoracle.render_range(hs.desc, 16, 24, nthreads=8)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    rgb_got, rgb_ref = hs.resolve(got), hs.resolve(ref)
+    assert _rmse(rgb_got, rgb_ref) / max(1.0, float(rgb_ref.mean())) < 1e-4
+
+
+def test_tile_groups_batching_equal(variant):
+    """Batches of whole tiles (several groups) and of sample chunks inside a
+    tile must reproduce the single-batch film bit for bit where the batch
+    holds whole tiles, and within float rounding otherwise."""
+    path = variant(res=(80, 40), spp=8)
+    hs = ptgpu.HostScene(path)
+    one, _ = ptgpu.Scene(hs).render_accum(0, 1)
+    groups, _ = ptgpu.Scene(hs, batch_slots=16 * 16 * 8 * 3).render_accum(0, 1)   # 3 tiles per batch
+    assert np.array_equal(one.view(np.uint32), groups.view(np.uint32))
+    chunks, _ = ptgpu.Scene(hs, batch_slots=16 * 16 * 3).render_accum(0, 1)       # 3 samples per batch
+    np.testing.assert_allclose(chunks, one, rtol=1e-5, atol=1e-6)
