@@ -280,6 +280,11 @@ pt_status pt_film_size_host(const pt_scene_desc* desc, int32_t* width, int32_t* 
 pt_status pt_render_accum(pt_scene* scene, int tile_offset, int tile_stride,
                           float* accum_out, pt_stats* stats);
 
+/* Same as pt_render_range but synchronous, into a host buffer. */
+pt_status pt_render_range_accum(pt_scene* scene, int tile_offset, int tile_stride,
+                                int sample_begin, int sample_end, float* accum_out,
+                                pt_stats* stats);
+
 /* Number of in-flight paths per wavefront batch (default 8M).  Memory for
  * path state is ~230 bytes per slot. */
 pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);

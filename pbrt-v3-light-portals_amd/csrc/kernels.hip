@@ -210,7 +210,8 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
     const uint32_t N = (uint32_t)ps.n;
     const uint32_t total = (uint32_t)npix * (uint32_t)nsamp;
     for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
-        const uint32_t sl = slot / (uint32_t)npix, p = slot - sl * (uint32_t)npix;
+        // pixel-major: a pixel's samples are consecutive slots (k_film loads them coalesced)
+        const uint32_t p = slot / (uint32_t)nsamp, sl = slot - p * (uint32_t)nsamp;
         const int2 px = pix[p];
         const uint32_t off = halton_pixel_offset(sc, px.x, px.y, hp.exp1, hp.scale0, hp.mi0, hp.mi1);
         const uint32_t idx = off + (uint32_t)(s0 + (int)sl) * sc.hal_stride;
@@ -603,14 +604,25 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps,
 // in tile order as XYZ (Film::MergeFilmTile film.cpp:117-130).  A pure
 // gather: deterministic, no float atomics.  Bit-identical to the reference
 // whenever a batch holds all samples of its tiles.
+//
+// One wave per film pixel: the 64 lanes evaluate 64 consecutive samples of a
+// source pixel (slots are pixel-major, so the loads coalesce), then the
+// touching lanes' contributions are added in lane order with readlane --
+// the float sum keeps the reference's sequential association.
 // ----------------------------------------------------------------------------
+__device__ __forceinline__ float lane_val(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
 __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
                                               int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum) {
     const uint32_t N = (uint32_t)ps.n;
     const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
     const int total = bw * bh;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int lane = (int)lane_id();
+    const int nwaves = (int)(gridDim.x * blockDim.x) >> 6;
+    for (int t = (int)(blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < total; t += nwaves) {
         const int tx = bx0 + t % bw, ty = by0 + t / bw;
         const int wy0 = max(ty - fc.win, fc.sb_y0), wy1 = min(ty + fc.win, fc.sb_y1 - 1);
         const int wx0 = max(tx - fc.win, fc.sb_x0), wx1 = min(tx + fc.win, fc.sb_x1 - 1);
@@ -624,46 +636,61 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
             for (int tc = tx0; tc <= tx1; ++tc) {
                 const int qy0 = max(wy0, fc.sb_y0 + 16 * tr), qy1 = min(wy1, fc.sb_y0 + 16 * tr + 15);
                 const int qx0 = max(wx0, fc.sb_x0 + 16 * tc), qx1 = min(wx1, fc.sb_x0 + 16 * tc + 15);
-                S3 part = s3(0.f);
-                float wsum = 0.f;
+                float p0s = 0.f, p1s = 0.f, p2s = 0.f, wsum = 0.f;
                 bool any = false;
                 for (int qy = qy0; qy <= qy1; ++qy) {
                     for (int qx = qx0; qx <= qx1; ++qx) {
                         const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
                         if (p < 0 || p >= np) continue;
-                        for (int sl = 0; sl < nsamp; ++sl) {
-                            const uint32_t slot = (uint32_t)sl * (uint32_t)np + (uint32_t)p;
-                            const float2 pf = ps.pfilm[slot];
-                            const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
-                            const int x0 = (int)ceilf(dx - fc.rx), x1 = (int)floorf(dx + fc.rx) + 1;
-                            const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
-                            if (tx < x0 || tx >= x1 || ty < y0 || ty >= y1) continue;
-                            S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
-                            if (has_nan(L)) L = s3(0.f);
-                            else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
-                            else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
-                            if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
-                            const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
-                            const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
-                            int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
-                            int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
-                            const float w = fc.table[iy * 16 + ix];
-                            part = part + (L * 1.f) * w;
-                            wsum += w;
-                            any = true;
+                        for (int c0 = 0; c0 < nsamp; c0 += 64) {
+                            const int sl = c0 + lane;
+                            bool touch = false;
+                            S3 c = s3(0.f);
+                            float w = 0.f;
+                            if (sl < nsamp) {
+                                const uint32_t slot = (uint32_t)p * (uint32_t)nsamp + (uint32_t)sl;
+                                const float2 pf = ps.pfilm[slot];
+                                const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
+                                const int x0 = (int)ceilf(dx - fc.rx), x1 = (int)floorf(dx + fc.rx) + 1;
+                                const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
+                                touch = !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
+                                if (touch) {
+                                    S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                                    if (has_nan(L)) L = s3(0.f);
+                                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
+                                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
+                                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                                    const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
+                                    const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
+                                    int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                                    int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                                    w = fc.table[iy * 16 + ix];
+                                    c = (L * 1.f) * w;
+                                }
+                            }
+                            uint64_t m = __ballot(touch);
+                            if (m) any = true;
+                            while (m) {
+                                const int j = __ffsll((unsigned long long)m) - 1;
+                                m &= m - 1;
+                                p0s += lane_val(c.c[0], j);
+                                p1s += lane_val(c.c[1], j);
+                                p2s += lane_val(c.c[2], j);
+                                wsum += lane_val(w, j);
+                            }
                         }
                     }
                 }
                 if (!any) continue;
                 // RGBSpectrum::ToXYZ (spectrum.h:64-68) of the tile pixel, merged
-                acc.x += 0.412453f * part.c[0] + 0.357580f * part.c[1] + 0.180423f * part.c[2];
-                acc.y += 0.212671f * part.c[0] + 0.715160f * part.c[1] + 0.072169f * part.c[2];
-                acc.z += 0.019334f * part.c[0] + 0.119193f * part.c[1] + 0.950227f * part.c[2];
+                acc.x += 0.412453f * p0s + 0.357580f * p1s + 0.180423f * p2s;
+                acc.y += 0.212671f * p0s + 0.715160f * p1s + 0.072169f * p2s;
+                acc.z += 0.019334f * p0s + 0.119193f * p1s + 0.950227f * p2s;
                 acc.w += wsum;
                 touched = true;
             }
         }
-        if (touched) accum[o] = acc;
+        if (touched && lane == 0) accum[o] = acc;
     }
 }
 

@@ -680,7 +680,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             }
             const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
             if (bw > 0 && bh > 0) {
-                hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(bw * bh, 256), s->num_cus * 16))),
+                hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32))),
                                    dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
                                    d_accum);
                 HIPCHK(hipGetLastError());
@@ -884,16 +884,29 @@ pt_status pt_render_range(pt_scene* s, int tile_offset, int tile_stride, int sam
     });
 }
 
+static void render_to_host(pt_scene* s, int tile_offset, int tile_stride, int s_begin, int s_end, float* accum_out,
+                           pt_stats* stats) {
+    size_t np = (size_t)s->fr.width() * s->fr.height();
+    DBuf<float4> acc;
+    acc.alloc(np);
+    HIPCHK(hipMemset(acc.p, 0, np * sizeof(float4)));
+    RenderResult r = render_tiles(s, tile_offset, tile_stride, s_begin, s_end, acc.p, nullptr);
+    HIPCHK(hipMemcpy(accum_out, acc.p, np * sizeof(float4), hipMemcpyDeviceToHost));
+    fill_stats(r, stats);
+}
+
 pt_status pt_render_accum(pt_scene* s, int tile_offset, int tile_stride, float* accum_out, pt_stats* stats) {
     return guarded([&] {
         if (!s || !accum_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
-        size_t np = (size_t)s->fr.width() * s->fr.height();
-        DBuf<float4> acc;
-        acc.alloc(np);
-        HIPCHK(hipMemset(acc.p, 0, np * sizeof(float4)));
-        RenderResult r = render_tiles(s, tile_offset, tile_stride, 0, s->spp, acc.p, nullptr);
-        HIPCHK(hipMemcpy(accum_out, acc.p, np * sizeof(float4), hipMemcpyDeviceToHost));
-        fill_stats(r, stats);
+        render_to_host(s, tile_offset, tile_stride, 0, s->spp, accum_out, stats);
+    });
+}
+
+pt_status pt_render_range_accum(pt_scene* s, int tile_offset, int tile_stride, int sample_begin, int sample_end,
+                                float* accum_out, pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !accum_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        render_to_host(s, tile_offset, tile_stride, sample_begin, sample_end, accum_out, stats);
     });
 }
 

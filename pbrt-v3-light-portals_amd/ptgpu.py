@@ -70,6 +70,8 @@ def lib() -> ctypes.CDLL:
     L.pt_film_size.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_render.argtypes = [vp, f32p, ctypes.POINTER(pt_stats)]
     L.pt_render_accum.argtypes = [vp, ctypes.c_int, ctypes.c_int, f32p, ctypes.POINTER(pt_stats)]
+    L.pt_render_range_accum.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p,
+                                        ctypes.POINTER(pt_stats)]
     L.pt_render_tiles.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(pt_stats)]
     L.pt_render_range.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
                                   ctypes.POINTER(pt_stats)]
@@ -181,6 +183,16 @@ class Scene:
         acc = np.zeros((h, w, 4), np.float32)
         st = pt_stats()
         _check(lib().pt_render_accum(self._s, tile_offset, tile_stride, _fptr(acc), ctypes.byref(st)))
+        return acc, st.as_dict()
+
+    def render_range(self, sample_begin: int, sample_end: int, tile_offset: int = 0,
+                     tile_stride: int = 1) -> Tuple[np.ndarray, dict]:
+        """Film (h, w, 4) for camera-sample indices [sample_begin, sample_end)."""
+        w, h = self.film_size()
+        acc = np.zeros((h, w, 4), np.float32)
+        st = pt_stats()
+        _check(lib().pt_render_range_accum(self._s, tile_offset, tile_stride, sample_begin, sample_end, _fptr(acc),
+                                           ctypes.byref(st)))
         return acc, st.as_dict()
 
     def render_tiles_device(self, tile_offset: int, tile_stride: int, d_accum: int, stream: int = 0) -> dict:

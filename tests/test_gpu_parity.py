@@ -1,7 +1,9 @@
 """GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on
 the same inputs.  Integer / index results must be bit-exact; radiance must
 match within the north_star tolerance (per-pixel RMSE < 1e-4 of the image,
-relative to its mean for the unbounded 'projection' estimator)."""
+relative to its mean for the unbounded 'projection' estimator) -- and the
+renders are in fact required to be bit-identical, since the device performs
+the oracle's float operations in the oracle's order."""
 import numpy as np
 import pytest
 
@@ -121,10 +123,10 @@ def test_render_matches_oracle(variant, strategy):
     exact = float(np.mean(np.all(got.view(np.uint32) == ref.view(np.uint32), axis=2)))
     print(f"{strategy}: rmse={rmse:.3g} mean={ref.mean():.5g} bit-exact pixels={exact:.4f} "
           f"rays gpu={gst['closest_rays']}/{gst['shadow_rays']} oracle={rst['closest_rays']}/{rst['shadow_rays']}")
-    assert rmse / scale < 1e-4
-    assert exact > 0.99
-    assert gst["camera_rays"] == rst["camera_rays"]
-    assert abs(gst["closest_rays"] - rst["closest_rays"]) <= 1e-3 * rst["closest_rays"]
+    assert rmse / scale < 1e-4          # north_star tolerance
+    assert exact == 1.0                 # in fact bit-identical (same float ops, same order)
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
 
 
 def test_render_accum_tiles_partition(variant):
@@ -159,24 +161,17 @@ def test_film_accumulation_matches_oracle(variant):
     ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
     exact = float(np.mean(np.all(got.view(np.uint32) == ref.view(np.uint32), axis=2)))
     print(f"film: bit-exact pixels={exact:.4f} max|d|={np.abs(got - ref).max():.3g}")
-    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
-    assert exact > 0.99
+    assert exact == 1.0
 
 
 def test_sample_range_matches_oracle(variant):
     """pt_render_range (the bench's sharding unit) for samples [16, 24) --
     past the scene's spp, as rank 1 of a weak-scaled run renders them."""
-    import torch
     hs, sc = _scene(variant(**MINI))
-    w, h = sc.film_size()
-    acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
-    sc.render_range_device(0, 1, 16, 24, acc.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    got = acc.cpu().numpy()
-    ref, _ = pyoracle.render_range(hs.desc, 16, 24, nthreads=8)
-    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
-    rgb_got, rgb_ref = hs.resolve(got), hs.resolve(ref)
-    assert _rmse(rgb_got, rgb_ref) / max(1.0, float(rgb_ref.mean())) < 1e-4
+    got, gst = sc.render_range(16, 24)
+    ref, rst = pyoracle.render_range(hs.desc, 16, 24, nthreads=8)
+    assert gst["samples"] == rst["samples"] == 64 * 36 * 8
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 def test_tile_groups_batching_equal(variant):

@@ -210,3 +210,21 @@ def test_device_trig_port_matches_host_libm():
         fc[i] = cosf(float(xs[i]))
     assert np.array_equal(s_out[sel].view(np.uint32), fs[sel].view(np.uint32))
     assert np.array_equal(c_out[sel].view(np.uint32), fc[sel].view(np.uint32))
+
+
+def test_probe_c2_counters(tmp_path):
+    """The reference's own run of the draft C2 scene (tests/golden/probe_c2.json,
+    from SURVEY.md): same sample count, total rays to 3 significant figures
+    and rays/sample to 4 -- the light transport (path lengths, NEE rays,
+    Russian roulette) matches the reference."""
+    import json
+    import os
+    from conftest import scene_variant
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "probe_c2.json")))
+    hs = ptgpu.HostScene(scene_variant(tmp_path, res=tuple(g["resolution"]), spp=g["spp"]))
+    img, st = pyoracle.render(hs.desc, nthreads=8)
+    rays = st["closest_rays"] + st["shadow_rays"]
+    assert st["samples"] == g["samples"]
+    assert float("%.3g" % rays) == g["rays_total_3sf"]
+    assert round(rays / st["samples"], 2) == g["rays_per_sample"]
+    assert float((img.max(axis=2) == 0).mean()) <= g["black_pixel_fraction_max"]
