@@ -84,6 +84,22 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
             "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3)}
 
 
+def pmc_traffic(workload: str, kernel: str = "pt::k_trace"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, made by scripts/pmc_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench on
+    the same workload), or (None, None) when there is none."""
+    import glob
+    import re
+    files = glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json"))
+    files.sort(key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("workload") == workload and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,6 +160,9 @@ def main():
         total_samples, total_rays = float(agg["samples"]), float(agg["closest_rays"] + agg["shadow_rays"])
 
     if rank == 0:
+        workload = (f"portal Cornell (config 2) {w}x{h} @{spp}spp{'/rank' if args.shard == 'samples' else ''}, "
+                    f"path maxdepth 5, {args.shard}-sharded")
+        traffic, traffic_src = pmc_traffic(workload)
         alg_bytes = 32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]
         achieved = alg_bytes / (agg["trace_ms"] * 1e-3) / 1e9 if agg["trace_ms"] > 0 else 0.0
         out = {
@@ -159,15 +178,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)",
-            "config": {"workload": f"portal Cornell (config 2) {w}x{h} @{spp}spp"
-                                   f"{'/rank' if args.shard == 'samples' else ''}, path maxdepth 5, "
-                                   f"{args.shard}-sharded", "resolution": [w, h],
+            "config": {"workload": workload, "resolution": [w, h],
                        "frame_spp": shardmod.frame_samples(spp, world, args.shard),
                        "parallelism": f"{args.shard} x{world}"},
             "mrays_per_s": round(total_rays / dt / 1e6, 2),
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": round(traffic, 1) if traffic is not None else None,
+                         "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
                          "kernel": "k_trace", "algorithmic_bytes_per_launch": round(
                              alg_bytes / max(1, agg["trace_launches"]), 1),
                          "avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4)},
