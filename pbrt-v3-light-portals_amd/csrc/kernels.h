@@ -10,6 +10,7 @@ constexpr int kTraceBlock = 128;  // 2 waves; LDS stack = kStackLds * 128 * 4 B
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
 constexpr int kMaxPortals = 64;
+constexpr int kLdsSceneMax = 16384;  // bytes of BVH nodes + prim records staged in LDS by k_trace<true>
 
 // HaltonSampler constants for the per-pixel offset (halton.cpp:65-93)
 struct HaltonPixelConsts {

@@ -60,8 +60,9 @@ __device__ __forceinline__ void flush_stats(DevStats* s, unsigned long long cl, 
 // [entry][lane] layout) with a per-thread global spill for deeper trees.
 // ----------------------------------------------------------------------------
 template <bool kAny>
-__device__ __forceinline__ int traverse(const DevScene& sc, Ray ray, int (*stk)[kTraceBlock], int* spill,
-                                        unsigned long long* nodes, unsigned long long* prims) {
+__device__ __forceinline__ int traverse(const DevScene& sc, const float4* __restrict__ bnodes,
+                                        const float4* __restrict__ bprims, Ray ray, int (*stk)[kTraceBlock],
+                                        int* spill, unsigned long long* nodes, unsigned long long* prims) {
     const int tid = threadIdx.x;
     const V3 inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
     const bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
@@ -69,8 +70,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, Ray ray, int (*stk)[
     int toVisit = 0, cur = 0, hitPrim = -1;
     if (sc.n_nodes == 0) return -1;
     for (;;) {
-        const float4 a = sc.nodes[2 * cur];
-        const float4 b = sc.nodes[2 * cur + 1];
+        const float4 a = bnodes[2 * cur];
+        const float4 b = bnodes[2 * cur + 1];
         ++*nodes;
         // Bounds3::IntersectP(ray, invDir, dirIsNeg) (geometry.h:1584-1606)
         float tMin = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
@@ -101,8 +102,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, Ray ray, int (*stk)[
                 for (int i = 0; i < np; ++i) {
                     const int pi = off + i;
                     ++*prims;
-                    const float4 r0 = sc.prims[3 * pi];
-                    const float4 r1 = sc.prims[3 * pi + 1];
+                    const float4 r0 = bprims[3 * pi];
+                    const float4 r1 = bprims[3 * pi + 1];
                     const uint32_t fl = __float_as_uint(r0.w);
                     float t;
                     bool ok;
@@ -110,7 +111,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, Ray ray, int (*stk)[
                         V3 ph;
                         ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
                     } else {
-                        const float4 r2 = sc.prims[3 * pi + 2];
+                        const float4 r2 = bprims[3 * pi + 2];
                         float b0, b1, b2;
                         ok = tri_test(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t, &b0,
                                       &b1, &b2);
@@ -151,10 +152,24 @@ __device__ __forceinline__ void store_ray6(float* a, uint32_t n, uint32_t slot, 
     a[3 * n + slot] = r.d.x; a[4 * n + slot] = r.d.y; a[5 * n + slot] = r.d.z;
 }
 
+// kLdsScene: small scenes (nodes + prim records <= kLdsSceneMax bytes) are
+// staged once per block into LDS, so the dependent node/primitive fetches of
+// the traversal are LDS reads instead of L1/L2 round trips.
+template <bool kLdsScene>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                        const uint32_t* __restrict__ rq_count, int* spill,
                                                        DevStats* stats) {
     __shared__ int stk[kStackLds][kTraceBlock];
+    extern __shared__ float4 lds_scene[];
+    const float4* bnodes = sc.nodes;
+    const float4* bprims = sc.prims;
+    if constexpr (kLdsScene) {
+        const int nn = 2 * sc.n_nodes, total = nn + 3 * sc.n_prims;
+        for (int i = threadIdx.x; i < total; i += blockDim.x) lds_scene[i] = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        __syncthreads();
+        bnodes = lds_scene;
+        bprims = lds_scene + nn;
+    }
     const uint32_t n = *rq_count;
     const uint32_t N = (uint32_t)ps.n;
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -167,7 +182,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
             const float* a = ps.rayA;
             Ray r{v3(a[slot], a[N + slot], a[2 * N + slot]), v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
                   a[6 * N + slot]};
-            int h = traverse<true>(sc, r, stk, myspill, &nodes, &prims);
+            int h = traverse<true>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             ps.hitA[slot] = h >= 0 ? 1 : 0;
             ++nsh;
         } else {
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
             if (kind == kRayCont) r = load_ray6(ps.ray, N, slot, kInf);
             else if (kind == kRayA) r = load_ray6(ps.rayA, N, slot, kInf);
             else r = load_ray6(ps.rayB, N, slot, kInf);
-            int h = traverse<false>(sc, r, stk, myspill, &nodes, &prims);
+            int h = traverse<false>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             if (kind == kRayCont) ps.hit[slot] = h;
             else if (kind == kRayA) ps.hitA[slot] = h;
             else ps.hitB[slot] = h;
@@ -325,27 +340,33 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
     uint32_t flags = kNfPortal;
     if (l.strategy != PT_PORTAL_LIGHT) {
         const V3 pObj = xf_point(lp.w2o, it.p);
-        float dist[kMaxPortals];
-        float sum = 0;
-        bool behindAll = true;
-        for (int i = 0; i < l.n_portals; ++i) {
-            if (!plane_in_front(sc.portal_planes[l.first_portal + i], pObj)) { dist[i] = 0; continue; }
-            behindAll = false;
-            dist[i] = 1;  // InFrustum() is always true (aaportal.cpp:101-104)
-            sum += dist[i];
-        }
-        if (!behindAll) {
-            if (sum == 0) { put_nee(ps, slot, kNeeFlags, __uint_as_float(flags)); return false; }
-            const int np = l.n_portals;
-            for (int i = 0; i < np; ++i) dist[i] /= sum;
-            float cdf[kMaxPortals + 1];
-            cdf[0] = 0;
-            for (int i = 1; i < np + 1; ++i) cdf[i] = cdf[i - 1] + dist[i - 1] / np;
-            const float funcInt = cdf[np];
-            if (funcInt == 0) { for (int i = 1; i < np + 1; ++i) cdf[i] = (float)i / (float)np; }
-            else { for (int i = 1; i < np + 1; ++i) cdf[i] /= funcInt; }
-            const int sel = find_interval(cdf, np + 1, u10);
-            const float portalPdf = (funcInt > 0) ? dist[sel] / (funcInt * np) : 0;
+        // Distribution1D over the portals' visibility (portal_arealight.cpp:38-60),
+        // evaluated without arrays: InFrustum() is always true (aaportal.cpp:101-104),
+        // so dist[i] is 1 for portals in front of the point and 0 otherwise; the
+        // CDF entries are recomputed with the same sequential float sums.
+        const int np = l.n_portals;
+        const DevPlane* portals = sc.portal_planes + l.first_portal;
+        int nvis = 0;
+        for (int i = 0; i < np; ++i) nvis += plane_in_front(portals[i], pObj) ? 1 : 0;
+        if (nvis > 0) {
+            float sum = 0;
+            for (int i = 0; i < nvis; ++i) sum += 1.f;
+            const float dv = 1.f / sum;            // dist[i] /= sum
+            const float inc = dv / (float)np;      // Distribution1D: func[i] / n
+            float funcInt = 0;
+            for (int i = 0; i < np; ++i) funcInt = funcInt + (plane_in_front(portals[i], pObj) ? inc : 0.f / (float)np);
+            // FindInterval over the monotone CDF = number of entries <= u, minus one
+            int cnt = 1;  // cdf[0] = 0 <= u
+            float c = 0;
+            for (int i = 1; i < np + 1; ++i) {
+                c = c + (plane_in_front(portals[i - 1], pObj) ? inc : 0.f / (float)np);
+                const float ci = funcInt == 0 ? (float)i / (float)np : c / funcInt;
+                cnt += ci <= u10 ? 1 : 0;
+            }
+            int sel = cnt - 1;
+            sel = sel < 0 ? 0 : (sel > np - 1 ? np - 1 : sel);
+            const float dsel = plane_in_front(portals[sel], pObj) ? dv : 0.f / sum;
+            const float portalPdf = (funcInt > 0) ? dsel / (funcInt * np) : 0;
             const DevPlane& pp = sc.portal_planes[l.first_portal + sel];
             if (plane_in_front(pp, pObj)) {
                 V3 wi = v3(0, 0, 0);
@@ -571,10 +592,10 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
     *keep = (st & (kStCont | kStNee)) != 0;
 }
 
-__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
-                                                       const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-                                                       uint32_t* rq_out_count, uint32_t* pq_out,
-                                                       uint32_t* pq_out_count, DevStats* stats) {
+__device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& ps, const uint32_t* __restrict__ pq,
+                                            const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                            uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
+                                            DevStats* stats) {
     const uint32_t n = *pq_count;
     bool overflow = false;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
@@ -593,6 +614,25 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps,
         if (keep) pq_out[ppos] = slot;
     }
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
+}
+
+// Register-budget variants of the shading kernel (occupancy vs spills);
+// render.hip picks one (PT_SHADE_VARIANT).
+__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
+                                                       const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                                       uint32_t* rq_out_count, uint32_t* pq_out,
+                                                       uint32_t* pq_out_count, DevStats* stats) {
+    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_w4(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 
 // ----------------------------------------------------------------------------
@@ -723,7 +763,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_debug_trace(DevScene sc, const 
           rays[7 * i + 6]};
     unsigned long long a = 0, b = 0;
     int* sp = spill + (size_t)i * (64 - kStackLds);
-    out_prim[i] = any ? traverse<true>(sc, r, stk, sp, &a, &b) : traverse<false>(sc, r, stk, sp, &a, &b);
+    out_prim[i] = any ? traverse<true>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b)
+                      : traverse<false>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b);
 }
 
 }  // namespace pt

@@ -8,6 +8,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -193,6 +194,8 @@ struct pt_scene {
     int device = 0;
     int num_cus = 256;
     size_t target_slots = (size_t)8 << 20;
+    size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
+    int shade_variant = 0;       // 0: compiler register budget, 3/4: forced waves per SIMD
 };
 
 namespace pt {
@@ -658,16 +661,20 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 if (nrays > 0) {
                     auto e = tev_get(tcount++);
                     HIPCHK(hipEventRecord(e.first, stream));
-                    hipLaunchKernelGGL(k_trace,
-                                       dim3(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace))),
-                                       dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in, counts + 0, w.spill.p,
-                                       w.stats.p);
+                    const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
+                    if (s->lds_scene_bytes)
+                        hipLaunchKernelGGL(k_trace<true>, tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
+                                           ps, rq_in, counts + 0, w.spill.p, w.stats.p);
+                    else
+                        hipLaunchKernelGGL(k_trace<false>, tg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
+                                           counts + 0, w.spill.p, w.stats.p);
                     HIPCHK(hipEventRecord(e.second, stream));
                     rr.launches++;
                 }
-                hipLaunchKernelGGL(k_shade, dim3(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade))),
-                                   dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out, counts + 2,
-                                   pq_out, counts + 3, w.stats.p);
+                const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
+                auto kshade = s->shade_variant == 4 ? k_shade_w4 : (s->shade_variant == 3 ? k_shade_w3 : k_shade);
+                hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out,
+                                   counts + 2, pq_out, counts + 3, w.stats.p);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
@@ -826,6 +833,14 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         HIPCHK(hipGetDeviceProperties(&prop, s->device));
         s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
         build_scene(s.get(), desc);
+        // kernel variants: LDS-resident BVH for small scenes (PT_TRACE_LDS=0 disables),
+        // shading register budget (PT_SHADE_VARIANT=3|4)
+        const size_t scene_bytes = (2 * (size_t)s->dev.n_nodes + 3 * (size_t)s->dev.n_prims) * sizeof(float4);
+        const char* e = std::getenv("PT_TRACE_LDS");
+        s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
+                                 ? scene_bytes : 0;
+        const char* v = std::getenv("PT_SHADE_VARIANT");
+        s->shade_variant = v ? std::atoi(v) : 0;
         *out = s.release();
     });
 }
