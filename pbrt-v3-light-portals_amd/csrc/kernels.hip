@@ -201,6 +201,168 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
 }
 
 // ----------------------------------------------------------------------------
+// Persistent traversal with per-lane ray refill.  The same traversal as
+// traverse<kAny> (same node order, same box and primitive tests, same tMax
+// updates, same counters) restated as a one-step-per-iteration state machine:
+// each iteration a lane either visits one node or tests one primitive of the
+// leaf it reached, and a lane whose ray has finished takes the next ray of
+// the queue (one atomic per wave per refill) instead of idling until the
+// slowest ray of its wave is done.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2) {
+    // Bounds3::IntersectP(ray, invDir, dirIsNeg) (geometry.h:1584-1606)
+    const float kx = 1 + 2 * gammaf(3);
+    float tMin = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
+    float tMax = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
+    float tyMin = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
+    float tyMax = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
+    tMax *= kx;
+    tyMax *= kx;
+    if (tMin > tyMax || tyMin > tMax) return false;
+    if (tyMin > tMin) tMin = tyMin;
+    if (tyMax < tMax) tMax = tyMax;
+    float tzMin = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
+    float tzMax = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
+    tzMax *= kx;
+    if (tMin > tzMax || tzMin > tMax) return false;
+    if (tzMin > tMin) tMin = tzMin;
+    if (tzMax < tMax) tMax = tzMax;
+    return (tMin < ray.tmax) && (tMax > 0);
+}
+
+template <bool kLdsScene>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+                                                          const uint32_t* __restrict__ rq_count, uint32_t* fetch,
+                                                          int refill_min, int* spill, DevStats* stats) {
+    __shared__ int stk[kStackLds][kTraceBlock];
+    extern __shared__ float4 lds_scene[];
+    const float4* bnodes = sc.nodes;
+    const float4* bprims = sc.prims;
+    if constexpr (kLdsScene) {
+        const int nn = 2 * sc.n_nodes, total = nn + 3 * sc.n_prims;
+        for (int i = threadIdx.x; i < total; i += blockDim.x) lds_scene[i] = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        __syncthreads();
+        bnodes = lds_scene;
+        bprims = lds_scene + nn;
+    }
+    const uint32_t n = *rq_count;
+    const uint32_t N = (uint32_t)ps.n;
+    const int tid = threadIdx.x;
+    const uint32_t lane = lane_id();
+    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * (64 - kStackLds);
+    unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0;
+    bool active = false, exhausted = false;
+    uint32_t slot = 0, kind = 0;
+    Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
+    V3 inv = v3(0, 0, 0);
+    bool n0 = false, n1 = false, n2 = false;
+    int cur = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle > 0 && (nidle >= (uint32_t)refill_min || nidle == 64u)) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(fetch, nidle);
+                base = (uint32_t)__shfl((int)base, 0);
+                if (base + nidle >= n) exhausted = true;
+                if (!active) {
+                    const uint32_t i = base + (uint32_t)__popcll(idle & lower);
+                    if (i < n) {
+                        const uint32_t e = rq[i];
+                        slot = e >> 2;
+                        kind = e & 3u;
+                        const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
+                        ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
+                                  v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
+                                  kind == kRayShadow ? a[6 * N + slot] : kInf};
+                        inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                        n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
+                        cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
+                        active = true;
+                        if (kind == kRayShadow) ++nsh; else ++ncl;
+                    }
+                }
+            }
+        }
+        if (__ballot(active) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        if (!active) continue;
+        bool done = false;
+        if (sc.n_nodes == 0) {
+            done = true;
+        } else if (leafPos < leafEnd) {
+            const int pi = leafPos++;
+            ++prims;
+            const float4 r0 = bprims[3 * pi];
+            const float4 r1 = bprims[3 * pi + 1];
+            const uint32_t fl = __float_as_uint(r0.w);
+            float t;
+            bool ok;
+            if (fl & kPrimPlane) {
+                V3 ph;
+                ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+            } else {
+                const float4 r2 = bprims[3 * pi + 2];
+                float b0, b1, b2;
+                ok = tri_test(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t, &b0, &b1,
+                              &b2);
+                if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
+            }
+            if (ok) {
+                hitPrim = pi;
+                if (kind == kRayShadow) done = true;
+                else ray.tmax = t;
+            }
+            if (!done && leafPos == leafEnd) {
+                if (toVisit == 0) done = true;
+                else {
+                    --toVisit;
+                    cur = toVisit < kStackLds ? stk[toVisit][tid] : myspill[toVisit - kStackLds];
+                }
+            }
+        } else {
+            const float4 a = bnodes[2 * cur];
+            const float4 b = bnodes[2 * cur + 1];
+            ++nodes;
+            if (node_box_hit(a, b, ray, inv, n0, n1, n2)) {
+                const int off = __float_as_int(b.z);
+                const uint32_t npax = __float_as_uint(b.w);
+                const int np = (int)(npax & 0xffffu);
+                if (np > 0) {
+                    leafPos = off;
+                    leafEnd = off + np;
+                } else {
+                    const int axis = (int)(npax >> 16);
+                    const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                    const int far = neg ? cur + 1 : off;
+                    cur = neg ? off : cur + 1;
+                    if (toVisit < kStackLds) stk[toVisit][tid] = far;
+                    else myspill[toVisit - kStackLds] = far;
+                    ++toVisit;
+                }
+            } else if (toVisit == 0) {
+                done = true;
+            } else {
+                --toVisit;
+                cur = toVisit < kStackLds ? stk[toVisit][tid] : myspill[toVisit - kStackLds];
+            }
+        }
+        if (done) {
+            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
+            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
+            else ps.hitB[slot] = hitPrim;
+            active = false;
+        }
+    }
+    flush_stats(stats, ncl, nsh, nodes, prims);
+}
+
+// ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
 // (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
 // ----------------------------------------------------------------------------

@@ -196,6 +196,9 @@ struct pt_scene {
     size_t target_slots = (size_t)8 << 20;
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int shade_variant = 0;       // 0: compiler register budget, 3/4: forced waves per SIMD
+    int trace_persist = 1;       // k_trace_pt (per-lane refill) instead of k_trace
+    int trace_bpc = 12;          // persistent trace blocks per CU
+    int refill_min = 1;          // idle lanes that trigger a refill
 };
 
 namespace pt {
@@ -662,7 +665,17 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     auto e = tev_get(tcount++);
                     HIPCHK(hipEventRecord(e.first, stream));
                     const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
-                    if (s->lds_scene_bytes)
+                    if (s->trace_persist) {
+                        // persistent: about one resident wave set; lanes refill from counts[4]
+                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+                        if (s->lds_scene_bytes)
+                            hipLaunchKernelGGL(k_trace_pt<true>, pg, dim3(kTraceBlock), s->lds_scene_bytes, stream,
+                                               s->dev, ps, rq_in, counts + 0, counts + 4, s->refill_min, w.spill.p,
+                                               w.stats.p);
+                        else
+                            hipLaunchKernelGGL(k_trace_pt<false>, pg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
+                                               counts + 0, counts + 4, s->refill_min, w.spill.p, w.stats.p);
+                    } else if (s->lds_scene_bytes)
                         hipLaunchKernelGGL(k_trace<true>, tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
                                            ps, rq_in, counts + 0, w.spill.p, w.stats.p);
                     else
@@ -841,6 +854,9 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                  ? scene_bytes : 0;
         const char* v = std::getenv("PT_SHADE_VARIANT");
         s->shade_variant = v ? std::atoi(v) : 0;
+        if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
+        if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::atoi(t));
+        if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
         *out = s.release();
     });
 }
