@@ -233,7 +233,7 @@ __device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray,
 template <bool kLdsScene>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
-                                                          int refill_min, int* spill, DevStats* stats) {
+                                                          int refill_min, int leaf_min, int* spill, DevStats* stats) {
     __shared__ int stk[kStackLds][kTraceBlock];
     extern __shared__ float4 lds_scene[];
     const float4* bnodes = sc.nodes;
@@ -290,7 +290,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
             if (exhausted) break;
             continue;
         }
-        if (!active) continue;
+        // One uniform step kind per iteration: primitive tests for the lanes
+        // parked at a leaf once at least leaf_min of them are (or no lane has
+        // a node to visit), otherwise node visits for the others.  A lane's
+        // own sequence of node visits and primitive tests is unchanged.
+        const bool wantLeaf = active && leafPos < leafEnd;
+        const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wantLeaf));
+        const uint32_t nNode = (uint32_t)__popcll(__ballot(active && !wantLeaf));
+        const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        if (!active || wantLeaf != leafStep) continue;
         bool done = false;
         if (sc.n_nodes == 0) {
             done = true;

@@ -198,7 +198,8 @@ struct pt_scene {
     int shade_variant = 0;       // 0: compiler register budget, 3/4: forced waves per SIMD
     int trace_persist = 1;       // k_trace_pt (per-lane refill) instead of k_trace
     int trace_bpc = 12;          // persistent trace blocks per CU
-    int refill_min = 1;          // idle lanes that trigger a refill
+    int refill_min = 64;         // idle lanes that trigger a refill (64: whole-wave refill)
+    int leaf_min = 1;            // lanes parked at leaves that trigger a primitive-test step
 };
 
 namespace pt {
@@ -670,11 +671,11 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         if (s->lds_scene_bytes)
                             hipLaunchKernelGGL(k_trace_pt<true>, pg, dim3(kTraceBlock), s->lds_scene_bytes, stream,
-                                               s->dev, ps, rq_in, counts + 0, counts + 4, s->refill_min, w.spill.p,
+                                               s->dev, ps, rq_in, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.spill.p,
                                                w.stats.p);
                         else
                             hipLaunchKernelGGL(k_trace_pt<false>, pg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
-                                               counts + 0, counts + 4, s->refill_min, w.spill.p, w.stats.p);
+                                               counts + 0, counts + 4, s->refill_min, s->leaf_min, w.spill.p, w.stats.p);
                     } else if (s->lds_scene_bytes)
                         hipLaunchKernelGGL(k_trace<true>, tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
                                            ps, rq_in, counts + 0, w.spill.p, w.stats.p);
@@ -857,6 +858,7 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
         if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::atoi(t));
         if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
+        if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
         *out = s.release();
     });
 }
