@@ -210,47 +210,53 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
 // slowest ray of its wave is done.
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2) {
-    // Bounds3::IntersectP(ray, invDir, dirIsNeg) (geometry.h:1584-1606)
+    // Bounds3::IntersectP(ray, invDir, dirIsNeg) (geometry.h:1584-1606), its
+    // early exits folded into one predicate (same values, no branches)
     const float kx = 1 + 2 * gammaf(3);
     float tMin = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
     float tMax = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
-    float tyMin = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
+    const float tyMin = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
     float tyMax = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
+    const float tzMin = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
+    float tzMax = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
     tMax *= kx;
     tyMax *= kx;
-    if (tMin > tyMax || tyMin > tMax) return false;
-    if (tyMin > tMin) tMin = tyMin;
-    if (tyMax < tMax) tMax = tyMax;
-    float tzMin = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
-    float tzMax = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
     tzMax *= kx;
-    if (tMin > tzMax || tzMin > tMax) return false;
-    if (tzMin > tMin) tMin = tzMin;
-    if (tzMax < tMax) tMax = tzMax;
-    return (tMin < ray.tmax) && (tMax > 0);
+    const bool ok1 = !(tMin > tyMax) & !(tyMin > tMax);
+    tMin = tyMin > tMin ? tyMin : tMin;
+    tMax = tyMax < tMax ? tyMax : tMax;
+    const bool ok2 = !(tMin > tzMax) & !(tzMin > tMax);
+    tMin = tzMin > tMin ? tzMin : tMin;
+    tMax = tzMax < tMax ? tzMax : tMax;
+    return ok1 & ok2 & (tMin < ray.tmax) & (tMax > 0);
 }
 
-template <bool kLdsScene>
+template <bool kLdsScene, bool kSpill>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
-                                                          int refill_min, int leaf_min, int* spill, DevStats* stats) {
-    __shared__ int stk[kStackLds][kTraceBlock];
-    extern __shared__ float4 lds_scene[];
+                                                          int refill_min, int leaf_min, int stack_rows, int* spill,
+                                                          DevStats* stats) {
+    // Dynamic LDS: [scene float4s if kLdsScene][stack].  With kSpill the
+    // stack is kStackLds entries per lane plus a global spill; without, the
+    // BVH is shallow enough that stack_rows entries per lane always suffice.
+    extern __shared__ float4 lds_dyn[];
     const float4* bnodes = sc.nodes;
     const float4* bprims = sc.prims;
+    const int scene_f4 = kLdsScene ? 2 * sc.n_nodes + 3 * sc.n_prims : 0;
     if constexpr (kLdsScene) {
-        const int nn = 2 * sc.n_nodes, total = nn + 3 * sc.n_prims;
-        for (int i = threadIdx.x; i < total; i += blockDim.x) lds_scene[i] = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        const int nn = 2 * sc.n_nodes;
+        for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) lds_dyn[i] = i < nn ? sc.nodes[i] : sc.prims[i - nn];
         __syncthreads();
-        bnodes = lds_scene;
-        bprims = lds_scene + nn;
+        bnodes = lds_dyn;
+        bprims = lds_dyn + nn;
     }
+    int* stk = (int*)(lds_dyn + scene_f4);  // [row][kTraceBlock]
     const uint32_t n = *rq_count;
     const uint32_t N = (uint32_t)ps.n;
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
     const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * (64 - kStackLds);
+    int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
     unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0;
     bool active = false, exhausted = false;
     uint32_t slot = 0, kind = 0;
@@ -280,7 +286,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
                         cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
-                        active = true;
+                        active = sc.n_nodes > 0;  // empty scene: every ray misses
+                        if (!active) {
+                            if (kind == kRayShadow) ps.hitA[slot] = 0;
+                            else if (kind == kRayCont) ps.hit[slot] = -1;
+                            else if (kind == kRayA) ps.hitA[slot] = -1;
+                            else ps.hitB[slot] = -1;
+                        }
                         if (kind == kRayShadow) ++nsh; else ++ncl;
                     }
                 }
@@ -300,9 +312,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
         const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
         if (!active || wantLeaf != leafStep) continue;
         bool done = false;
-        if (sc.n_nodes == 0) {
-            done = true;
-        } else if (leafPos < leafEnd) {
+        if (leafStep) {
             const int pi = leafPos++;
             ++prims;
             const float4 r0 = bprims[3 * pi];
@@ -329,7 +339,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                 if (toVisit == 0) done = true;
                 else {
                     --toVisit;
-                    cur = toVisit < kStackLds ? stk[toVisit][tid] : myspill[toVisit - kStackLds];
+                    cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
                 }
             }
         } else {
@@ -348,15 +358,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                     const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
                     const int far = neg ? cur + 1 : off;
                     cur = neg ? off : cur + 1;
-                    if (toVisit < kStackLds) stk[toVisit][tid] = far;
-                    else myspill[toVisit - kStackLds] = far;
+                    if (!kSpill || toVisit < stack_rows) stk[toVisit * kTraceBlock + tid] = far;
+                    else myspill[toVisit - stack_rows] = far;
                     ++toVisit;
                 }
             } else if (toVisit == 0) {
                 done = true;
             } else {
                 --toVisit;
-                cur = toVisit < kStackLds ? stk[toVisit][tid] : myspill[toVisit - kStackLds];
+                cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
             }
         }
         if (done) {

@@ -156,7 +156,7 @@ struct Work {
             rayB.alloc(6 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
             cap = n;
         }
-        spill.alloc(spill_threads * (64 - kStackLds));
+        spill.alloc(spill_threads * 64);
         counts.alloc(8);
         stats.alloc(1);
     }
@@ -197,9 +197,11 @@ struct pt_scene {
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int shade_variant = 0;       // 0: compiler register budget, 3/4: forced waves per SIMD
     int trace_persist = 1;       // k_trace_pt (per-lane refill) instead of k_trace
-    int trace_bpc = 12;          // persistent trace blocks per CU
-    int refill_min = 64;         // idle lanes that trigger a refill (64: whole-wave refill)
-    int leaf_min = 1;            // lanes parked at leaves that trigger a primitive-test step
+    int trace_bpc = 16;          // persistent trace blocks per CU
+    int refill_min = 48;         // idle lanes that trigger a refill (64: whole-wave refill)
+    int leaf_min = 32;           // lanes parked at leaves that trigger a primitive-test step
+    int trace_spill = 1;         // BVH deeper than the LDS stack: keep the global spill path
+    int stack_rows = pt::kStackLds;  // LDS stack entries per lane in k_trace_pt
 };
 
 namespace pt {
@@ -628,7 +630,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     const int maxBlocksTrace = s->num_cus * 16;
     const int maxBlocksShade = s->num_cus * 8;
     Work& w = s->work;
-    w.ensure(max_slots, (size_t)maxBlocksTrace * kTraceBlock);
+    w.ensure(max_slots, (size_t)std::max(maxBlocksTrace, s->num_cus * s->trace_bpc) * kTraceBlock);
     HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
     DevPaths ps = w.paths((int)max_slots);
     hipEvent_t ev0, ev1;
@@ -669,13 +671,12 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     if (s->trace_persist) {
                         // persistent: about one resident wave set; lanes refill from counts[4]
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-                        if (s->lds_scene_bytes)
-                            hipLaunchKernelGGL(k_trace_pt<true>, pg, dim3(kTraceBlock), s->lds_scene_bytes, stream,
-                                               s->dev, ps, rq_in, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.spill.p,
-                                               w.stats.p);
-                        else
-                            hipLaunchKernelGGL(k_trace_pt<false>, pg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
-                                               counts + 0, counts + 4, s->refill_min, s->leaf_min, w.spill.p, w.stats.p);
+                        auto kt = s->lds_scene_bytes ? (s->trace_spill ? k_trace_pt<true, true> : k_trace_pt<true, false>)
+                                                     : (s->trace_spill ? k_trace_pt<false, true> : k_trace_pt<false, false>);
+                        const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
+                        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0,
+                                           counts + 4, s->refill_min, s->leaf_min, s->stack_rows, w.spill.p,
+                                           w.stats.p);
                     } else if (s->lds_scene_bytes)
                         hipLaunchKernelGGL(k_trace<true>, tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
                                            ps, rq_in, counts + 0, w.spill.p, w.stats.p);
@@ -837,6 +838,23 @@ pt_status pt_init(int device) {
     });
 }
 
+// Deepest traversal stack the flattened BVH can need: interior nodes on the
+// longest root-to-leaf path (each pushes one entry).
+static int bvh_stack_bound(const std::vector<LinearNode>& nodes) {
+    if (nodes.empty()) return 0;
+    int best = 0;
+    std::vector<std::pair<int, int>> todo{{0, 0}};
+    while (!todo.empty()) {
+        auto [i, d] = todo.back();
+        todo.pop_back();
+        if (i < 0 || i >= (int)nodes.size()) continue;
+        if (nodes[i].nprims > 0) { best = std::max(best, d); continue; }
+        todo.push_back({i + 1, d + 1});
+        todo.push_back({nodes[i].offset, d + 1});
+    }
+    return best;
+}
+
 pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     return guarded([&] {
         if (!out) throw PtError(PT_ERR_INVALID_ARG, "null out");
@@ -847,6 +865,13 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         HIPCHK(hipGetDeviceProperties(&prop, s->device));
         s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
         build_scene(s.get(), desc);
+        const int sbound = bvh_stack_bound(s->host_nodes);
+        s->trace_spill = sbound > kStackLds;
+        s->stack_rows = s->trace_spill ? kStackLds : std::max(1, sbound);
+        if (const char* t = std::getenv("PT_STACK_ROWS")) {  // test hook: force the spill path
+            s->stack_rows = std::max(1, std::min(kStackLds, std::atoi(t)));
+            s->trace_spill = sbound > s->stack_rows;
+        }
         // kernel variants: LDS-resident BVH for small scenes (PT_TRACE_LDS=0 disables),
         // shading register budget (PT_SHADE_VARIANT=3|4)
         const size_t scene_bytes = (2 * (size_t)s->dev.n_nodes + 3 * (size_t)s->dev.n_prims) * sizeof(float4);
@@ -856,7 +881,7 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         const char* v = std::getenv("PT_SHADE_VARIANT");
         s->shade_variant = v ? std::atoi(v) : 0;
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
-        if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::atoi(t));
+        if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
         if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
         if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
         *out = s.release();

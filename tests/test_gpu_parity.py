@@ -185,3 +185,17 @@ def test_tile_groups_batching_equal(variant):
     assert np.array_equal(one.view(np.uint32), groups.view(np.uint32))
     chunks, _ = ptgpu.Scene(hs, batch_slots=16 * 16 * 3).render_accum(0, 1)       # 3 samples per batch
     np.testing.assert_allclose(chunks, one, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_LDS": "0"}])
+def test_trace_variants_bit_exact(variant, monkeypatch, env):
+    """Every traversal variant the driver can pick -- LDS stack with global
+    spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
+    global-memory BVH -- renders the oracle's image bit for bit."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    hs, sc = _scene(variant(**MINI))
+    got, gst = sc.render()
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst["node_visits"] == rst["node_visits"]
