@@ -133,7 +133,9 @@ struct DevStats {
     unsigned long long nodes;
     unsigned long long prims;
     unsigned long long dim_overflow;
-    unsigned long long pad[3];
+    unsigned long long lane_iters;  // k_trace_pt: lane-iterations executed (SIMD slots)
+    unsigned long long lane_steps;  // k_trace_pt: node visits + primitive tests performed
+    unsigned long long pad;
 };
 
 }  // namespace pt

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
     const uint32_t lane = lane_id();
     const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
-    unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0;
+    unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
     bool active = false, exhausted = false;
     uint32_t slot = 0, kind = 0;
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
@@ -310,6 +310,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
         const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wantLeaf));
         const uint32_t nNode = (uint32_t)__popcll(__ballot(active && !wantLeaf));
         const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        ++iters;
         if (!active || wantLeaf != leafStep) continue;
         bool done = false;
         if (leafStep) {
@@ -378,6 +379,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
         }
     }
     flush_stats(stats, ncl, nsh, nodes, prims);
+    iters = wave_sum_u64(iters);
+    if (lane == 0 && iters) atomicAdd(&stats->lane_iters, iters);
 }
 
 // ----------------------------------------------------------------------------

@@ -729,6 +729,10 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
     if (rr.st.dim_overflow) throw PtError(PT_ERR_UNSUPPORTED, "Halton dimension table exhausted");
+    if (std::getenv("PT_TRACE_DEBUG") && rr.st.lane_iters)
+        std::fprintf(stderr, "[pt] trace SIMD utilisation %.3f (%llu steps / %llu lane-iterations)\n",
+                     (double)(rr.st.nodes + rr.st.prims) / (double)rr.st.lane_iters,
+                     (unsigned long long)(rr.st.nodes + rr.st.prims), (unsigned long long)rr.st.lane_iters);
     return rr;
 }
 
