@@ -123,6 +123,60 @@ __device__ __forceinline__ bool tri_test(V3 p0, V3 p1, V3 p2, const Ray& ray, fl
     return true;
 }
 
+// Accept/reject + t of tri_test, written for SIMD execution: the same float
+// operations in the same order, the early exits folded into one predicate
+// (only the rare double-precision edge recomputation stays a branch).
+__device__ __forceinline__ bool tri_hit(V3 p0, V3 p1, V3 p2, const Ray& ray, float* tHit) {
+    V3 p0t = p0 - ray.o, p1t = p1 - ray.o, p2t = p2 - ray.o;
+    const int kz = maxdim(vabs(ray.d));
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    const V3 d = permute(ray.d, kx, ky, kz);
+    p0t = permute(p0t, kx, ky, kz);
+    p1t = permute(p1t, kx, ky, kz);
+    p2t = permute(p2t, kx, ky, kz);
+    const float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1.f / d.z;
+    p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
+    float e0 = p1t.x * p2t.y - p1t.y * p2t.x;
+    float e1 = p2t.x * p0t.y - p2t.y * p0t.x;
+    float e2 = p0t.x * p1t.y - p0t.y * p1t.x;
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double p2txp1ty = (double)p2t.x * (double)p1t.y;
+        double p2typ1tx = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(p2typ1tx - p2txp1ty);
+        double p0txp2ty = (double)p0t.x * (double)p2t.y;
+        double p0typ2tx = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(p0typ2tx - p0txp2ty);
+        double p1txp0ty = (double)p1t.x * (double)p0t.y;
+        double p1typ0tx = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(p1typ0tx - p1txp0ty);
+    }
+    bool ok = !((e0 < 0 || e1 < 0 || e2 < 0) & (e0 > 0 || e1 > 0 || e2 > 0));
+    const float det = e0 + e1 + e2;
+    ok &= det != 0;
+    p0t.z *= Sz; p1t.z *= Sz; p2t.z *= Sz;
+    const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    const float tmd = ray.tmax * det;
+    ok &= !((det < 0) & ((tScaled >= 0) | (tScaled < tmd)));
+    ok &= !((det > 0) & ((tScaled <= 0) | (tScaled > tmd)));
+    const float invDet = 1 / det;
+    const float t = tScaled * invDet;
+    const float maxZt = maxcomp(vabs(v3(p0t.z, p1t.z, p2t.z)));
+    const float deltaZ = gammaf(3) * maxZt;
+    const float maxXt = maxcomp(vabs(v3(p0t.x, p1t.x, p2t.x)));
+    const float maxYt = maxcomp(vabs(v3(p0t.y, p1t.y, p2t.y)));
+    const float deltaX = gammaf(5) * (maxXt + maxZt);
+    const float deltaY = gammaf(5) * (maxYt + maxZt);
+    const float deltaE = 2 * (gammaf(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    const float maxE = maxcomp(vabs(v3(e0, e1, e2)));
+    const float deltaT = 3 * (gammaf(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * fabsf(invDet);
+    ok &= !(t <= deltaT);
+    *tHit = t;
+    return ok;
+}
+
 // ----------------------------------------------------------------------------
 // AAPlaneShape::Intersect (plane.cpp:15-55) -- test part
 // ----------------------------------------------------------------------------

@@ -384,6 +384,147 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
 }
 
 // ----------------------------------------------------------------------------
+// k_trace_nb: k_trace_pt with the per-step control flow replaced by selects
+// (the traversal is the same; only which instructions run changes).  The
+// stack push is an unconditional LDS store above the top; the pop an
+// unconditional LDS load below it.  Only for BVHs whose stack fits in LDS.
+// ----------------------------------------------------------------------------
+template <bool kLdsScene>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+                                                          const uint32_t* __restrict__ rq_count, uint32_t* fetch,
+                                                          int refill_min, int leaf_min, DevStats* stats) {
+    extern __shared__ float4 lds_dyn[];
+    const float4* bnodes = sc.nodes;
+    const float4* bprims = sc.prims;
+    const int scene_f4 = kLdsScene ? 2 * sc.n_nodes + 3 * sc.n_prims : 0;
+    if constexpr (kLdsScene) {
+        const int nn = 2 * sc.n_nodes;
+        for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) lds_dyn[i] = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        __syncthreads();
+        bnodes = lds_dyn;
+        bprims = lds_dyn + nn;
+    }
+    int* stk = (int*)(lds_dyn + scene_f4) + threadIdx.x;  // entry k at stk[k * kTraceBlock]
+    const uint32_t n = *rq_count;
+    const uint32_t N = (uint32_t)ps.n;
+    const uint32_t lane = lane_id();
+    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
+    bool active = false, exhausted = false;
+    uint32_t slot = 0, kind = 0;
+    Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
+    V3 inv = v3(0, 0, 0);
+    bool n0 = false, n1 = false, n2 = false;
+    int cur = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(fetch, nidle);
+                base = (uint32_t)__shfl((int)base, 0);
+                if (base + nidle >= n) exhausted = true;
+                if (!active) {
+                    const uint32_t i = base + (uint32_t)__popcll(idle & lower);
+                    if (i < n) {
+                        const uint32_t e = rq[i];
+                        slot = e >> 2;
+                        kind = e & 3u;
+                        const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
+                        ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
+                                  v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
+                                  kind == kRayShadow ? a[6 * N + slot] : kInf};
+                        inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                        n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
+                        cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
+                        active = sc.n_nodes > 0;  // empty scene: every ray misses
+                        if (!active) {
+                            if (kind == kRayShadow) ps.hitA[slot] = 0;
+                            else if (kind == kRayCont) ps.hit[slot] = -1;
+                            else if (kind == kRayA) ps.hitA[slot] = -1;
+                            else ps.hitB[slot] = -1;
+                        }
+                        if (kind == kRayShadow) ++nsh; else ++ncl;
+                    }
+                }
+            }
+        }
+        const bool wantLeaf = active && leafPos < leafEnd;
+        const uint64_t mLeaf = __ballot(wantLeaf);
+        const uint64_t mNode = __ballot(active && !wantLeaf);
+        if ((mLeaf | mNode) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        ++iters;
+        bool done = false;
+        if (leafStep) {
+            if (wantLeaf) {
+                const int pi = leafPos++;
+                ++prims;
+                const float4 r0 = bprims[3 * pi];
+                const float4 r1 = bprims[3 * pi + 1];
+                const float4 r2 = bprims[3 * pi + 2];
+                const uint32_t fl = __float_as_uint(r0.w);
+                float t = 0;
+                bool ok;
+                if (fl & kPrimPlane) {
+                    V3 ph;
+                    ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+                } else {
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t);
+                    ok &= (kind == kRayShadow) | !(fl & kPrimDegenerate);
+                }
+                hitPrim = ok ? pi : hitPrim;
+                ray.tmax = (ok && kind != kRayShadow) ? t : ray.tmax;
+                done = ok && kind == kRayShadow;
+                const bool leafDone = !done && leafPos == leafEnd;
+                const int popv = stk[max(toVisit - 1, 0) * kTraceBlock];
+                done |= leafDone && toVisit == 0;
+                const bool pop = leafDone && toVisit > 0;
+                cur = pop ? popv : cur;
+                toVisit -= pop ? 1 : 0;
+            }
+        } else if (active && !wantLeaf) {
+            const int c = cur;
+            const float4 a = bnodes[2 * c];
+            const float4 b = bnodes[2 * c + 1];
+            ++nodes;
+            const bool hit = node_box_hit(a, b, ray, inv, n0, n1, n2);
+            const int off = __float_as_int(b.z);
+            const uint32_t npax = __float_as_uint(b.w);
+            const int np = (int)(npax & 0xffffu);
+            const int axis = (int)(npax >> 16);
+            const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+            const bool inner = hit && np == 0;
+            const bool leaf = hit && np > 0;
+            const bool miss = !hit;
+            stk[toVisit * kTraceBlock] = neg ? c + 1 : off;  // push slot (kept only for an inner node)
+            const int popv = stk[max(toVisit - 1, 0) * kTraceBlock];
+            const bool pop = miss && toVisit > 0;
+            done = miss && toVisit == 0;
+            cur = inner ? (neg ? off : c + 1) : (pop ? popv : c);
+            toVisit += inner ? 1 : (pop ? -1 : 0);
+            leafPos = leaf ? off : leafPos;
+            leafEnd = leaf ? off + np : leafEnd;
+        }
+        if (done) {
+            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
+            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
+            else ps.hitB[slot] = hitPrim;
+            active = false;
+        }
+    }
+    flush_stats(stats, ncl, nsh, nodes, prims);
+    const unsigned long long it = wave_sum_u64(iters);
+    if (lane == 0 && it) atomicAdd(&stats->lane_iters, it);
+}
+
+// ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
 // (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
 // ----------------------------------------------------------------------------

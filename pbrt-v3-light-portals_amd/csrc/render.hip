@@ -668,7 +668,14 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     auto e = tev_get(tcount++);
                     HIPCHK(hipEventRecord(e.first, stream));
                     const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
-                    if (s->trace_persist) {
+                    if (s->trace_persist == 2 && !s->trace_spill) {
+                        // branch-reduced persistent traversal; LDS stack of depth+1 rows
+                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+                        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
+                        hipLaunchKernelGGL(s->lds_scene_bytes ? k_trace_nb<true> : k_trace_nb<false>, pg,
+                                           dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0, counts + 4,
+                                           s->refill_min, s->leaf_min, w.stats.p);
+                    } else if (s->trace_persist) {
                         // persistent: about one resident wave set; lanes refill from counts[4]
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         auto kt = s->lds_scene_bytes ? (s->trace_spill ? k_trace_pt<true, true> : k_trace_pt<true, false>)

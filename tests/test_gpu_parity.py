@@ -187,7 +187,9 @@ def test_tile_groups_batching_equal(variant):
     np.testing.assert_allclose(chunks, one, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_LDS": "0"}])
+@pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
+                                 {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
