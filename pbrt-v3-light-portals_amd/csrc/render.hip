@@ -195,11 +195,11 @@ struct pt_scene {
     int num_cus = 256;
     size_t target_slots = (size_t)8 << 20;
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
-    int shade_variant = 0;       // 0: compiler register budget, 3/4: forced waves per SIMD
-    int trace_persist = 1;       // k_trace_pt (per-lane refill) instead of k_trace
+    int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
+    int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
-    int refill_min = 48;         // idle lanes that trigger a refill (64: whole-wave refill)
-    int leaf_min = 32;           // lanes parked at leaves that trigger a primitive-test step
+    int refill_min = 64;         // idle lanes that trigger a refill (64: whole-wave refill)
+    int leaf_min = 16;           // lanes parked at leaves that trigger a primitive-test step
     int trace_spill = 1;         // BVH deeper than the LDS stack: keep the global spill path
     int stack_rows = pt::kStackLds;  // LDS stack entries per lane in k_trace_pt
 };
@@ -890,7 +890,7 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                                  ? scene_bytes : 0;
         const char* v = std::getenv("PT_SHADE_VARIANT");
-        s->shade_variant = v ? std::atoi(v) : 0;
+        if (v) s->shade_variant = std::atoi(v);
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
         if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
         if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
