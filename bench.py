@@ -84,8 +84,9 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
             "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3)}
 
 
-def pmc_traffic(workload: str, kernel: str = "pt::k_trace"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+def pmc_traffic(workload: str, kernel: str = "k_trace"):
+    """HBM bytes per launch of the traversal kernel (name containing `kernel`;
+    the variant with the most launches) from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, made by scripts/pmc_summary.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench on
     the same workload), or (None, None) when there is none."""
@@ -95,8 +96,11 @@ def pmc_traffic(workload: str, kernel: str = "pt::k_trace"):
     files.sort(key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
     for f in reversed(files):
         d = json.load(open(f))
-        if d.get("workload") == workload and kernel in d.get("kernels", {}):
-            return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(f, REPO)
+        if d.get("workload") != workload:
+            continue
+        ks = [(v["launches"], v["hbm_bytes_per_launch"]) for k, v in d.get("kernels", {}).items() if kernel in k]
+        if ks:
+            return max(ks)[1], os.path.relpath(f, REPO)
     return None, None
 
 
