@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -58,7 +58,8 @@ enum pt_prim_kind { PT_PRIM_TRIANGLE = 0, PT_PRIM_AAPLANE = 1 };
 
 enum pt_material_kind {
     PT_MAT_NONE = 0,   /* "" / "none": null BSDF, path passes through   */
-    PT_MAT_MATTE = 1   /* MatteMaterial  src/materials/matte.cpp:45-62 */
+    PT_MAT_MATTE = 1,  /* MatteMaterial  src/materials/matte.cpp:45-62 */
+    PT_MAT_METAL = 2   /* MetalMaterial  src/materials/metal.cpp:58-79 */
 };
 
 enum pt_light_kind {
@@ -116,9 +117,13 @@ typedef struct pt_prim {
 } pt_prim;
 
 typedef struct pt_material {
-    int32_t kind;   /* pt_material_kind */
-    float kd[3];    /* constant Kd (already Clamp()ed is NOT assumed) */
-    float sigma;    /* OrenNayar sigma in degrees; only 0 supported */
+    int32_t kind;    /* pt_material_kind */
+    float kd[3];     /* matte: constant Kd (Clamp() is applied by the renderer) */
+    float sigma;     /* matte: OrenNayar sigma in degrees; only 0 supported */
+    float eta[3];    /* metal: constant eta */
+    float k[3];      /* metal: constant k */
+    float alpha[2];  /* metal: TrowbridgeReitz alphax, alphay (after RoughnessToAlpha
+                        when remaproughness, and the 0.001 floor of the ctor) */
 } pt_material;
 
 /* AAPortal (src/portals/aaportal.h) as parsed from portalData. */
@@ -308,6 +313,11 @@ pt_status pt_debug_camera_rays(pt_scene* scene, int n, const float* film_xy, flo
 /* BVH traversal for rays (o, d, tMax): closest primitive index in BVH order
  * (any = 0) or occlusion flag (any = 1); -1 for a miss. */
 pt_status pt_debug_trace(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim);
+/* BSDF::f / Pdf / Sample_f of scene material `material` in the local shading
+ * frame (n = (0,0,1)): per record in8 = wo[3], wi[3], u0, u1 and
+ * out8 = f[3], pdf, sampled wi[3], sampled pdf (f is the sampled f when wi
+ * is all zero).  src/core/reflection.cpp:713-829. */
+pt_status pt_debug_bsdf(pt_scene* scene, int material, int n, const float* in8, float* out8);
 
 #ifdef __cplusplus
 }

@@ -1115,22 +1115,141 @@ static int scene_intersect_p(const Scene* sc, const Ray* ray, Counters* ctr) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* BSDF (core/reflection.{h,cpp}, materials/matte.cpp)                       */
+/* Microfacet distribution and Fresnel (core/microfacet.{h,cpp},             */
+/* core/reflection.{h,cpp})                                                  */
+/* ------------------------------------------------------------------------ */
+static float clampf11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); } /* Clamp (pbrt.h:309-316) */
+static float cos2t(V3 w) { return w.z * w.z; }                               /* reflection.h:57-90 */
+static float sin2t(V3 w) { return fmaxs((float)0, (float)1 - cos2t(w)); }
+static float sint(V3 w) { return sqrtf(sin2t(w)); }
+static float tant(V3 w) { return sint(w) / w.z; }
+static float tan2t(V3 w) { return sin2t(w) / cos2t(w); }
+static float cosp(V3 w) { float st = sint(w); return (st == 0) ? 1 : clampf11(w.x / st); }
+static float sinp(V3 w) { float st = sint(w); return (st == 0) ? 0 : clampf11(w.y / st); }
+static float cos2p(V3 w) { return cosp(w) * cosp(w); }
+static float sin2p(V3 w) { return sinp(w) * sinp(w); }
+
+static float trD(float ax, float ay, V3 wh) { /* microfacet.cpp:155-163 */
+    float tan2Theta = tan2t(wh);
+    if (isinf(tan2Theta)) return 0.;
+    const float cos4Theta = cos2t(wh) * cos2t(wh);
+    float e = (cos2p(wh) / (ax * ax) + sin2p(wh) / (ay * ay)) * tan2Theta;
+    return 1 / (PI_F * ax * ay * cos4Theta * (1 + e) * (1 + e));
+}
+static float trLambda(float ax, float ay, V3 w) { /* microfacet.cpp:176-184 */
+    float absTanTheta = fabsf(tant(w));
+    if (isinf(absTanTheta)) return 0.;
+    float alpha = sqrtf(cos2p(w) * ax * ax + sin2p(w) * ay * ay);
+    float alpha2Tan2Theta = (alpha * absTanTheta) * (alpha * absTanTheta);
+    return (-1 + sqrtf(1.f + alpha2Tan2Theta)) / 2;
+}
+static float trG1(float ax, float ay, V3 w) { return 1 / (1 + trLambda(ax, ay, w)); } /* microfacet.h:54-57 */
+static float trG(float ax, float ay, V3 wo, V3 wi) { return 1 / (1 + trLambda(ax, ay, wo) + trLambda(ax, ay, wi)); }
+
+/* microfacet.cpp:238-282; the normal-incidence branch uses <math.h>'s double
+ * sqrt/cos/sin, which the reference's unqualified calls resolve to. */
+static void trSample11(float cosTheta, float U1, float U2, float* slope_x, float* slope_y) {
+    if (cosTheta > .9999) {
+        float r = (float)sqrt((double)(U1 / (1 - U1)));
+        float phi = (float)(6.28318530718 * U2);
+        *slope_x = (float)(r * cos((double)phi));
+        *slope_y = (float)(r * sin((double)phi));
+        return;
+    }
+    float sinTheta = sqrtf(fmaxs((float)0, (float)1 - cosTheta * cosTheta));
+    float tanTheta = sinTheta / cosTheta;
+    float a = 1 / tanTheta;
+    float G1 = 2 / (1 + sqrtf(1.f + 1.f / (a * a)));
+    float A = 2 * U1 / G1 - 1;
+    float tmp = 1.f / (A * A - 1.f);
+    if (tmp > 1e10) tmp = (float)1e10;
+    float B = tanTheta;
+    float D = sqrtf(fmaxs((float)(B * B * tmp * tmp - (A * A - B * B) * tmp), (float)0));
+    float slope_x_1 = B * tmp - D;
+    float slope_x_2 = B * tmp + D;
+    *slope_x = (A < 0 || slope_x_2 > 1.f / tanTheta) ? slope_x_1 : slope_x_2;
+    float S;
+    if (U2 > 0.5f) { S = 1.f; U2 = 2.f * (U2 - .5f); }
+    else { S = -1.f; U2 = 2.f * (.5f - U2); }
+    float z = (U2 * (U2 * (U2 * 0.27385f - 0.73369f) + 0.46341f)) /
+              (U2 * (U2 * (U2 * 0.093073f + 0.309420f) - 1.000000f) + 0.597999f);
+    *slope_y = S * z * sqrtf(1.f + *slope_x * *slope_x);
+}
+static V3 trSample(V3 wi, float alpha_x, float alpha_y, float U1, float U2) { /* microfacet.cpp:284-305 */
+    V3 wiStretched = vnorm(v3(alpha_x * wi.x, alpha_y * wi.y, wi.z));
+    float slope_x, slope_y;
+    trSample11(wiStretched.z, U1, U2, &slope_x, &slope_y);
+    float tmp = cosp(wiStretched) * slope_x - sinp(wiStretched) * slope_y;
+    slope_y = sinp(wiStretched) * slope_x + cosp(wiStretched) * slope_y;
+    slope_x = tmp;
+    slope_x = alpha_x * slope_x;
+    slope_y = alpha_y * slope_y;
+    return vnorm(v3(-slope_x, -slope_y, 1.));
+}
+static V3 trSampleWh(float ax, float ay, V3 wo, const float* u) { /* microfacet.cpp:307-336, visible area */
+    int flip = wo.z < 0;
+    V3 wh = trSample(flip ? vneg(wo) : wo, ax, ay, u[0], u[1]);
+    if (flip) wh = vneg(wh);
+    return wh;
+}
+static float trPdf(float ax, float ay, V3 wo, V3 wh) { /* microfacet.cpp:338-345 */
+    return trD(ax, ay, wh) * trG1(ax, ay, wo) * vabsdot(wo, wh) / fabsf(wo.z);
+}
+static RGB sdiv(RGB a, RGB b) { RGB r = {{a.c[0] / b.c[0], a.c[1] / b.c[1], a.c[2] / b.c[2]}}; return r; }
+static RGB ssub(RGB a, RGB b) { RGB r = {{a.c[0] - b.c[0], a.c[1] - b.c[1], a.c[2] - b.c[2]}}; return r; }
+static RGB ssqrt(RGB a) { RGB r = {{sqrtf(a.c[0]), sqrtf(a.c[1]), sqrtf(a.c[2])}}; return r; }
+/* FrConductor (reflection.cpp:71-96) */
+static RGB frConductor(float cosThetaI, RGB etai, RGB etat, RGB k) {
+    cosThetaI = clampf11(cosThetaI);
+    RGB eta = sdiv(etat, etai);
+    RGB etak = sdiv(k, etai);
+    float cosThetaI2 = cosThetaI * cosThetaI;
+    float sinThetaI2 = (float)(1. - cosThetaI2);
+    RGB eta2 = smul(eta, eta);
+    RGB etak2 = smul(etak, etak);
+    RGB t0 = ssub(ssub(eta2, etak2), rgb1(sinThetaI2));
+    RGB a2plusb2 = ssqrt(sadd(smul(t0, t0), smul(smulf(eta2, 4), etak2)));
+    RGB t1 = sadd(a2plusb2, rgb1(cosThetaI2));
+    RGB a = ssqrt(smulf(sadd(a2plusb2, t0), 0.5f));
+    RGB t2 = smulf(a, (float)2 * cosThetaI);
+    RGB Rs = sdiv(ssub(t1, t2), sadd(t1, t2));
+    RGB t3 = sadd(smulf(a2plusb2, cosThetaI2), rgb1(sinThetaI2 * sinThetaI2));
+    RGB t4 = smulf(t2, sinThetaI2);
+    RGB Rp = sdiv(smul(Rs, ssub(t3, t4)), sadd(t3, t4));
+    return smulf(sadd(Rp, Rs), 0.5f);
+}
+
+/* ------------------------------------------------------------------------ */
+/* BSDF (core/reflection.{h,cpp}; materials/matte.cpp, materials/metal.cpp)   */
 /* ------------------------------------------------------------------------ */
 typedef struct {
-    int nbxdf;       /* 0 or 1 LambertianReflection */
+    int nbxdf;       /* 0 or 1 BxDF */
+    int metal;       /* 0: LambertianReflection(R); 1: MicrofacetReflection(R=1, TR, FresnelConductor) */
     RGB R;
+    RGB eta, k;
+    float ax, ay;
     V3 ns, ng, ss, ts;
 } BSDF;
 
-/* MatteMaterial::ComputeScatteringFunctions (matte.cpp:45-62) + BSDF ctor (reflection.h:167-172) */
+/* MatteMaterial / MetalMaterial ::ComputeScatteringFunctions (matte.cpp:45-62,
+ * metal.cpp:58-79) + BSDF ctor (reflection.h:167-172) */
 static void make_bsdf(const pt_material* m, const SI* si, BSDF* b) {
     b->ns = si->sn; b->ng = si->n;
     b->ss = vnorm(si->sdpdu);
     b->ts = vcross(b->ns, b->ss);
+    b->nbxdf = 0;
+    b->metal = m->kind == PT_MAT_METAL;
+    if (b->metal) {
+        b->nbxdf = 1;
+        b->R = rgb1(1.);
+        b->eta = rgbv(m->eta);
+        b->k = rgbv(m->k);
+        b->ax = m->alpha[0];
+        b->ay = m->alpha[1];
+        return;
+    }
     RGB r = rgbv(m->kd);
     for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : (r.c[i] > INFINITY ? INFINITY : r.c[i]); /* Clamp() */
-    b->nbxdf = 0;
     if (!sblack(r)) { b->nbxdf = 1; b->R = r; }
 }
 static V3 w2l(const BSDF* b, V3 v) { return v3(vdot(v, b->ss), vdot(v, b->ts), vdot(v, b->ns)); }
@@ -1139,15 +1258,37 @@ static V3 l2w(const BSDF* b, V3 v) {
               b->ss.y * v.x + b->ts.y * v.y + b->ns.y * v.z,
               b->ss.z * v.x + b->ts.z * v.y + b->ns.z * v.z);
 }
-/* Lambertian is BSDF_REFLECTION|BSDF_DIFFUSE: matches both BSDF_ALL and
+/* MicrofacetReflection::f (reflection.cpp:259-271) */
+static RGB mf_f(const BSDF* b, V3 wo, V3 wi) {
+    float cosThetaO = fabsf(wo.z), cosThetaI = fabsf(wi.z);
+    V3 wh = vadd(wi, wo);
+    if (cosThetaI == 0 || cosThetaO == 0) return rgb1(0.);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return rgb1(0.);
+    wh = vnorm(wh);
+    V3 whf = vdot(wh, v3(0, 0, 1)) < 0.f ? vneg(wh) : wh; /* Faceforward */
+    RGB F = frConductor(fabsf(vdot(wi, whf)), rgb1(1.), b->eta, b->k); /* FresnelConductor::Evaluate */
+    return sdivf(smul(smulf(smulf(b->R, trD(b->ax, b->ay, wh)), trG(b->ax, b->ay, wo, wi)), F),
+                 4 * cosThetaI * cosThetaO);
+}
+static RGB bxdf_f(const BSDF* b, V3 wo, V3 wi) {
+    return b->metal ? mf_f(b, wo, wi) : smulf(b->R, INVPI_F);
+}
+static float bxdf_pdf(const BSDF* b, V3 wo, V3 wi) {
+    if (b->metal) { /* MicrofacetReflection::Pdf (reflection.cpp:458-462) */
+        if (!(wo.z * wi.z > 0)) return 0;
+        V3 wh = vnorm(vadd(wo, wi));
+        return trPdf(b->ax, b->ay, wo, wh) / (4 * vdot(wo, wh));
+    }
+    return (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0; /* BxDF::Pdf (reflection.cpp:425-427) */
+}
+/* Both BxDFs are non-specular reflection lobes: they match BSDF_ALL and
  * BSDF_ALL & ~BSDF_SPECULAR. */
 static RGB bsdf_f(const BSDF* b, V3 woW, V3 wiW) { /* reflection.cpp:713-726 */
     V3 wi = w2l(b, wiW), wo = w2l(b, woW);
-    (void)wi;
     if (wo.z == 0) return rgb1(0);
     int reflect = vdot(wiW, b->ng) * vdot(woW, b->ng) > 0;
     RGB f = rgb1(0);
-    if (b->nbxdf && reflect) f = sadd(f, smulf(b->R, INVPI_F));
+    if (b->nbxdf && reflect) f = sadd(f, bxdf_f(b, wo, wi));
     return f;
 }
 static float bsdf_pdf(const BSDF* b, V3 woW, V3 wiW) { /* reflection.cpp:814-829 */
@@ -1157,30 +1298,38 @@ static float bsdf_pdf(const BSDF* b, V3 woW, V3 wiW) { /* reflection.cpp:814-829
     float pdf = 0.f;
     int matching = 0;
     ++matching;
-    pdf += (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0;
+    pdf += bxdf_pdf(b, wo, wi);
     return matching > 0 ? pdf / matching : 0.f;
 }
-/* BSDF::Sample_f (reflection.cpp:747-812) with BxDF::Sample_f (416-423).
- * *pdf_set tells whether *pdf was written (it is not when wo.z == 0). */
+/* BSDF::Sample_f (reflection.cpp:747-812) with BxDF::Sample_f (416-423) or
+ * MicrofacetReflection::Sample_f (443-456). */
 static RGB bsdf_sample_f(const BSDF* b, V3 woW, V3* wiW, const float* u, float* pdf, int* sampled) {
     if (b->nbxdf == 0) { *pdf = 0; *sampled = 0; return rgb1(0); }
     int matchingComps = 1;
     int comp = (int)floorf(u[0] * matchingComps);
     if (comp > matchingComps - 1) comp = matchingComps - 1;
     float ur[2] = {fmins(u[0] * matchingComps - comp, ONE_MINUS_EPS), u[1]};
-    V3 wo = w2l(b, woW);
+    V3 wo = w2l(b, woW), wi;
     if (wo.z == 0) { *sampled = 0; return rgb1(0); }
     *pdf = 0;
     *sampled = 1;
-    V3 wi = cosine_sample_hemisphere(ur);
-    if (wo.z < 0) wi.z *= -1;
-    *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0;
-    RGB f = smulf(b->R, INVPI_F);
+    if (b->metal) {
+        if (wo.z == 0) return rgb1(0.);
+        V3 wh = trSampleWh(b->ax, b->ay, wo, ur);
+        if (vdot(wo, wh) < 0) return rgb1(0.);
+        wi = vadd(vneg(wo), vmul(wh, 2 * vdot(wo, wh))); /* Reflect (reflection.h:93-95) */
+        if (!(wo.z * wi.z > 0)) return rgb1(0.f);
+        *pdf = trPdf(b->ax, b->ay, wo, wh) / (4 * vdot(wo, wh));
+    } else {
+        wi = cosine_sample_hemisphere(ur);
+        if (wo.z < 0) wi.z *= -1;
+        *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0;
+    }
     if (*pdf == 0) { *sampled = 0; return rgb1(0); }
     *wiW = l2w(b, wi);
     int reflect = vdot(*wiW, b->ng) * vdot(woW, b->ng) > 0;
-    f = rgb1(0);
-    if (reflect) f = sadd(f, smulf(b->R, INVPI_F));
+    RGB f = rgb1(0);
+    if (reflect) f = sadd(f, bxdf_f(b, wo, wi));
     return f;
 }
 
@@ -1815,6 +1964,41 @@ int oracle_render_range(const pt_scene_desc* desc, float* accum_out, int nthread
     return render_common(desc, NULL, accum_out, nthreads, -1, tile_offset, tile_stride, s_begin, s_end, stats);
 }
 void oracle_set_trig(int correctly_rounded) { g_cr_trig = correctly_rounded; }
+
+/* BSDF of a material in the shading frame ns = ng = (0,0,1), ss = (1,0,0):
+ * f and pdf for (wo, wi), and Sample_f for (wo, u).  Known-answer hook. */
+static void local_bsdf(const pt_material* m, BSDF* b) {
+    SI si;
+    memset(&si, 0, sizeof si);
+    si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
+    make_bsdf(m, &si, b);
+}
+/* Batched BSDF hook with the layout of the product's pt_debug_bsdf: per record
+ * in8 = wo[3], wi[3], u0, u1 -> out8 = f[3], pdf, sampled wi[3], sampled pdf
+ * (f is the sampled f when wi is all zero). */
+int oracle_bsdf_batch(const pt_scene_desc* d, int mat, int n, const float* in8, float* out8) {
+    BSDF b;
+    if (!d || mat < 0 || mat >= d->n_materials) return 1;
+    local_bsdf(&d->materials[mat], &b);
+    for (int i = 0; i < n; ++i) {
+        const float* a = in8 + 8 * i;
+        float* o = out8 + 8 * i;
+        V3 wo = v3(a[0], a[1], a[2]), wi = v3(a[3], a[4], a[5]);
+        RGB f = rgb1(0);
+        float pdf = 0;
+        int zero = wi.x == 0 && wi.y == 0 && wi.z == 0;
+        if (!zero) { f = bsdf_f(&b, wo, wi); pdf = bsdf_pdf(&b, wo, wi); }
+        float u[2] = {a[6], a[7]};
+        V3 ws = v3(0, 0, 0);
+        float spdf = 0;
+        int sampled = 0;
+        RGB sf = bsdf_sample_f(&b, wo, &ws, u, &spdf, &sampled);
+        if (zero) f = sf;
+        o[0] = f.c[0]; o[1] = f.c[1]; o[2] = f.c[2]; o[3] = pdf;
+        o[4] = ws.x; o[5] = ws.y; o[6] = ws.z; o[7] = spdf;
+    }
+    return 0;
+}
 int oracle_film_size(const pt_scene_desc* desc, int* w, int* h) {
     Scene sc;
     memset(&sc, 0, sizeof sc);

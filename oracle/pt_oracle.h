@@ -70,6 +70,11 @@ int oracle_trace(const pt_scene_desc* desc, int n, const float* rays7, int any, 
 int oracle_build_bvh(const pt_scene_desc* desc, int32_t* n_nodes,
                      uint32_t* nodes, int32_t* prim_order, int32_t cap);
 
+/* BSDF of scene material `mat` in the local shading frame (n = (0,0,1)),
+ * batched like the product's pt_debug_bsdf: in8 = wo[3], wi[3], u0, u1 ->
+ * out8 = f[3], pdf, sampled wi[3], sampled pdf (f = sampled f when wi = 0). */
+int oracle_bsdf_batch(const pt_scene_desc* d, int mat, int n, const float* in8, float* out8);
+
 /* Known-answer helpers (src/core/lowdiscrepancy.cpp). */
 float oracle_radical_inverse(int base_index, uint64_t a);
 float oracle_scrambled_radical_inverse(int base_index, uint64_t a);

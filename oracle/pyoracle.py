@@ -46,6 +46,7 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(oracle_stats)]
         L.oracle_render_range.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.POINTER(oracle_stats)]
+        L.oracle_bsdf_batch.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
         L.oracle_set_trig.argtypes = [ctypes.c_int]
         L.oracle_set_trig.restype = None
         L.oracle_film_size.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -105,6 +106,15 @@ def render_range(desc: int, s_begin: int, s_end: int, nthreads: int = 1, tile_of
     lib().oracle_render_range(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride, s_begin,
                               s_end, ctypes.byref(st))
     return acc, st.as_dict()
+
+
+def bsdf_batch(desc: int, mat: int, rec8: np.ndarray) -> np.ndarray:
+    """BSDF::f / Pdf / Sample_f of material `mat` in the local frame n = (0,0,1):
+    (n, 8) records wo, wi, u0, u1 -> (n, 8) f, pdf, sampled wi, sampled pdf."""
+    rec8 = np.ascontiguousarray(rec8, np.float32)
+    out = np.zeros_like(rec8)
+    assert lib().oracle_bsdf_batch(ctypes.c_void_p(desc), mat, len(rec8), rec8.ctypes.data, out.ctypes.data) == 0
+    return out
 
 
 def build_bvh(desc: int) -> Tuple[np.ndarray, np.ndarray]:

@@ -205,7 +205,7 @@ __device__ __forceinline__ V3 vload3(const float* a, int i) { return v3(a[3 * i]
 // (triangle.cpp:297-420, interaction.cpp:44-89).  Returns false when the
 // reference would reject (it never does for the primitive that won in the
 // traversal, which already applied the same tests).
-__device__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si) {
+__device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si) {
     const pt_triangle tr = sc.tris[ti];
     V3 p0 = vload3(sc.P, tr.v[0]), p1 = vload3(sc.P, tr.v[1]), p2 = vload3(sc.P, tr.v[2]);
     Ray r2 = ray;
@@ -276,7 +276,7 @@ __device__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit*
 
 // Full AAPlaneShape::Intersect SurfaceInteraction, transformed to world space
 // (plane.cpp:35-50, transform.cpp:262-297).
-__device__ bool plane_surface(const DevPlane& pl, const Ray& ray, SurfHit* si) {
+__device__ __forceinline__ bool plane_surface(const DevPlane& pl, const Ray& ray, SurfHit* si) {
     Ray r2 = ray;
     r2.tmax = kInf;
     float t;
@@ -325,45 +325,194 @@ __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* mat
 // BSDF: MatteMaterial (matte.cpp:45-62) -> BSDF{LambertianReflection}
 // (reflection.h:167-213, reflection.cpp:211-213, 416-427, 713-829)
 // ----------------------------------------------------------------------------
+// ----------------------------------------------------------------------------
+// Shading-frame trigonometry (reflection.h:55-90) and the Trowbridge-Reitz
+// microfacet distribution (microfacet.h:105-133, microfacet.cpp:155-345)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float clamp11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); }
+__device__ __forceinline__ float cos2_theta(V3 w) { return w.z * w.z; }
+__device__ __forceinline__ float sin2_theta(V3 w) { return smax(0.f, 1.f - cos2_theta(w)); }
+__device__ __forceinline__ float sin_theta(V3 w) { return sqrtf(sin2_theta(w)); }
+__device__ __forceinline__ float tan_theta(V3 w) { return sin_theta(w) / w.z; }
+__device__ __forceinline__ float tan2_theta(V3 w) { return sin2_theta(w) / cos2_theta(w); }
+__device__ __forceinline__ float cos_phi(V3 w) {
+    const float st = sin_theta(w);
+    return (st == 0) ? 1.f : clamp11(w.x / st);
+}
+__device__ __forceinline__ float sin_phi(V3 w) {
+    const float st = sin_theta(w);
+    return (st == 0) ? 0.f : clamp11(w.y / st);
+}
+__device__ __forceinline__ float cos2_phi(V3 w) { return cos_phi(w) * cos_phi(w); }
+__device__ __forceinline__ float sin2_phi(V3 w) { return sin_phi(w) * sin_phi(w); }
+
+__device__ __forceinline__ float tr_D(float ax, float ay, V3 wh) {
+    const float t2 = tan2_theta(wh);
+    if (__builtin_isinf(t2)) return 0.f;
+    const float cos4 = cos2_theta(wh) * cos2_theta(wh);
+    const float e = (cos2_phi(wh) / (ax * ax) + sin2_phi(wh) / (ay * ay)) * t2;
+    return 1 / (kPi * ax * ay * cos4 * (1 + e) * (1 + e));
+}
+__device__ __forceinline__ float tr_lambda(float ax, float ay, V3 w) {
+    const float at = fabsf(tan_theta(w));
+    if (__builtin_isinf(at)) return 0.f;
+    const float alpha = sqrtf(cos2_phi(w) * ax * ax + sin2_phi(w) * ay * ay);
+    const float a2t2 = (alpha * at) * (alpha * at);
+    return (-1 + sqrtf(1.f + a2t2)) / 2;
+}
+__device__ __forceinline__ float tr_G1(float ax, float ay, V3 w) { return 1 / (1 + tr_lambda(ax, ay, w)); }
+__device__ __forceinline__ float tr_G(float ax, float ay, V3 wo, V3 wi) {
+    return 1 / (1 + tr_lambda(ax, ay, wo) + tr_lambda(ax, ay, wi));
+}
+// TrowbridgeReitzSample11 (microfacet.cpp:238-282).  The normal-incidence
+// branch calls the double-precision sqrt/cos/sin of <math.h> on float
+// arguments, as the reference's unqualified calls resolve.
+__device__ __forceinline__ void tr_sample11(float cosTheta, float U1, float U2, float* sx, float* sy) {
+    if ((double)cosTheta > .9999) {
+        const float r = (float)sqrt((double)(U1 / (1 - U1)));
+        const float phi = (float)(6.28318530718 * (double)U2);
+        *sx = (float)((double)r * dcos_mod((double)phi));
+        *sy = (float)((double)r * dsin_mod((double)phi));
+        return;
+    }
+    const float sinTheta = sqrtf(smax(0.f, 1.f - cosTheta * cosTheta));
+    const float tanTheta = sinTheta / cosTheta;
+    const float a = 1 / tanTheta;
+    const float G1 = 2 / (1 + sqrtf(1.f + 1.f / (a * a)));
+    const float A = 2 * U1 / G1 - 1;
+    float tmp = 1.f / (A * A - 1.f);
+    if ((double)tmp > 1e10) tmp = (float)1e10;
+    const float B = tanTheta;
+    const float D = sqrtf(smax(B * B * tmp * tmp - (A * A - B * B) * tmp, 0.f));
+    const float sx1 = B * tmp - D;
+    const float sx2 = B * tmp + D;
+    *sx = (A < 0 || sx2 > 1.f / tanTheta) ? sx1 : sx2;
+    float S;
+    if (U2 > 0.5f) { S = 1.f; U2 = 2.f * (U2 - .5f); }
+    else { S = -1.f; U2 = 2.f * (.5f - U2); }
+    const float z = (U2 * (U2 * (U2 * 0.27385f - 0.73369f) + 0.46341f)) /
+                    (U2 * (U2 * (U2 * 0.093073f + 0.309420f) - 1.000000f) + 0.597999f);
+    *sy = S * z * sqrtf(1.f + *sx * *sx);
+}
+__device__ __forceinline__ V3 tr_sample_wh(float ax, float ay, V3 wo, float u0, float u1) {  // visible normals
+    const bool flip = wo.z < 0;
+    const V3 wi = flip ? -wo : wo;
+    const V3 ws = normalize(v3(ax * wi.x, ay * wi.y, wi.z));
+    float sx, sy;
+    tr_sample11(ws.z, u0, u1, &sx, &sy);
+    const float tmp = cos_phi(ws) * sx - sin_phi(ws) * sy;
+    sy = sin_phi(ws) * sx + cos_phi(ws) * sy;
+    sx = tmp;
+    sx = ax * sx;
+    sy = ay * sy;
+    V3 wh = normalize(v3(-sx, -sy, 1.f));
+    if (flip) wh = -wh;
+    return wh;
+}
+__device__ __forceinline__ float tr_pdf(float ax, float ay, V3 wo, V3 wh) {  // MicrofacetDistribution::Pdf
+    return tr_D(ax, ay, wh) * tr_G1(ax, ay, wo) * absdot(wo, wh) / fabsf(wo.z);
+}
+// FrConductor with etaI = 1 (reflection.cpp:71-96)
+__device__ __forceinline__ S3 fr_conductor(float cosThetaI, S3 etat, S3 k) {
+    cosThetaI = clamp11(cosThetaI);
+    const S3 eta = etat / s3(1.f);
+    const S3 etak = k / s3(1.f);
+    const float c2 = cosThetaI * cosThetaI;
+    const float s2 = 1.f - c2;
+    const S3 eta2 = eta * eta, etak2 = etak * etak;
+    const S3 t0 = eta2 - etak2 - s3(s2);
+    const S3 a2b2 = ssqrt(t0 * t0 + (eta2 * 4.f) * etak2);
+    const S3 t1 = a2b2 + s3(c2);
+    const S3 a = ssqrt((a2b2 + t0) * 0.5f);
+    const S3 t2 = a * ((float)2 * cosThetaI);
+    const S3 Rs = (t1 - t2) / (t1 + t2);
+    const S3 t3 = a2b2 * c2 + s3(s2 * s2);
+    const S3 t4 = t2 * s2;
+    const S3 Rp = Rs * (t3 - t4) / (t3 + t4);
+    return (Rp + Rs) * 0.5f;
+}
+
+// ----------------------------------------------------------------------------
+// BSDF (reflection.{h,cpp}): one BxDF per material --
+//   matte: LambertianReflection(Kd)                     (matte.cpp:45-62)
+//   metal: MicrofacetReflection(1, TrowbridgeReitz, FresnelConductor(1, eta, k))
+//                                                       (metal.cpp:58-79)
+// ----------------------------------------------------------------------------
 struct Bsdf {
     int nbxdf;
+    int kind;            // PT_MAT_MATTE / PT_MAT_METAL
     S3 R;
+    const pt_material* m;
     V3 ns, ng, ss, ts;
 };
 
-__device__ __forceinline__ void make_bsdf(const pt_material& m, const SurfHit& si, Bsdf* b) {
+__device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, Bsdf* b) {
     b->ns = si.sn;
     b->ng = si.n;
     b->ss = normalize(si.sdpdu);
     b->ts = cross(b->ns, b->ss);
-    S3 r = s3(m.kd[0], m.kd[1], m.kd[2]);
-    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : r.c[i];  // Spectrum::Clamp()
-    b->nbxdf = is_black(r) ? 0 : 1;
-    b->R = r;
+    b->m = m;
+    b->kind = m->kind;
+    if (m->kind == PT_MAT_METAL) {
+        b->R = s3(1.f);
+        b->nbxdf = 1;
+    } else {
+        S3 r = s3(m->kd[0], m->kd[1], m->kd[2]);
+        for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : r.c[i];  // Spectrum::Clamp()
+        b->nbxdf = is_black(r) ? 0 : 1;
+        b->R = r;
+    }
 }
 __device__ __forceinline__ V3 w2l(const Bsdf& b, V3 v) { return v3(dot(v, b.ss), dot(v, b.ts), dot(v, b.ns)); }
 __device__ __forceinline__ V3 l2w(const Bsdf& b, V3 v) {
     return v3(b.ss.x * v.x + b.ts.x * v.y + b.ns.x * v.z, b.ss.y * v.x + b.ts.y * v.y + b.ns.y * v.z,
               b.ss.z * v.x + b.ts.z * v.y + b.ns.z * v.z);
 }
-__device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW) {
-    V3 wo = w2l(b, woW);
+// MicrofacetReflection::f (reflection.cpp:259-271), local frame
+__device__ __forceinline__ S3 mf_f(const Bsdf& b, V3 wo, V3 wi) {
+    const float cosO = fabsf(wo.z), cosI = fabsf(wi.z);
+    V3 wh = wi + wo;
+    if (cosI == 0 || cosO == 0) return s3(0.f);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return s3(0.f);
+    wh = normalize(wh);
+    const V3 whf = dot(wh, v3(0, 0, 1)) < 0.f ? -wh : wh;  // Faceforward(wh, (0,0,1))
+    const pt_material* m = b.m;
+    const S3 F = fr_conductor(fabsf(dot(wi, whf)), s3(m->eta[0], m->eta[1], m->eta[2]),
+                              s3(m->k[0], m->k[1], m->k[2]));
+    const float ax = m->alpha[0], ay = m->alpha[1];
+    return b.R * tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * F / (4 * cosI * cosO);
+}
+// BxDF::f of the material's one BxDF (local frame)
+__device__ __forceinline__ S3 bxdf_f(const Bsdf& b, V3 wo, V3 wi) {
+    if (b.kind == PT_MAT_METAL) return mf_f(b, wo, wi);
+    return b.R * kInvPi;
+}
+__device__ __forceinline__ float bxdf_pdf(const Bsdf& b, V3 wo, V3 wi) {
+    if (b.kind == PT_MAT_METAL) {  // MicrofacetReflection::Pdf (reflection.cpp:458-462)
+        if (!(wo.z * wi.z > 0)) return 0.f;
+        const V3 wh = normalize(wo + wi);
+        return tr_pdf(b.m->alpha[0], b.m->alpha[1], wo, wh) / (4 * dot(wo, wh));
+    }
+    return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;  // BxDF::Pdf (reflection.cpp:425-427)
+}
+__device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW) {  // BSDF::f (reflection.cpp:713-726)
+    V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return s3(0.f);
     bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
     S3 f = s3(0.f);
-    if (b.nbxdf && reflect) f = f + b.R * kInvPi;
+    if (b.nbxdf && reflect) f = f + bxdf_f(b, wo, wi);
     return f;
 }
-__device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW) {
+__device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW) {  // BSDF::Pdf (reflection.cpp:814-829)
     if (b.nbxdf == 0) return 0.f;
     V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return 0.f;
     float pdf = 0.f;
-    pdf += (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    pdf += bxdf_pdf(b, wo, wi);
     return pdf / 1;
 }
-// BSDF::Sample_f; returns false where the reference leaves *pdf unwritten
-// (wo.z == 0) -- f is black in that case.
+// BSDF::Sample_f (reflection.cpp:747-812); *pdf is left at 0 wherever the
+// reference returns black before writing it.
 __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf) {
     if (b.nbxdf == 0) { *pdf = 0; return s3(0.f); }
     int comp = (int)floorf(u0 * 1);
@@ -371,14 +520,27 @@ __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float 
     float ur0 = smin(u0 * 1 - comp, kOneMinusEps);
     V3 wo = w2l(b, woW);
     if (wo.z == 0) return s3(0.f);
-    V3 wi = cosine_sample_hemisphere(ur0, u1);
-    if (wo.z < 0) wi.z *= -1;
-    *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    *pdf = 0;
+    V3 wi;
+    if (b.kind == PT_MAT_METAL) {
+        // MicrofacetReflection::Sample_f (reflection.cpp:443-456)
+        const float ax = b.m->alpha[0], ay = b.m->alpha[1];
+        if (wo.z == 0) return s3(0.f);
+        const V3 wh = tr_sample_wh(ax, ay, wo, ur0, u1);
+        if (dot(wo, wh) < 0) return s3(0.f);
+        wi = -wo + (2 * dot(wo, wh)) * wh;  // Reflect
+        if (!(wo.z * wi.z > 0)) return s3(0.f);
+        *pdf = tr_pdf(ax, ay, wo, wh) / (4 * dot(wo, wh));
+    } else {
+        wi = cosine_sample_hemisphere(ur0, u1);
+        if (wo.z < 0) wi.z *= -1;
+        *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    }
     if (*pdf == 0) return s3(0.f);
     *wiW = l2w(b, wi);
     bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
     S3 f = s3(0.f);
-    if (reflect) f = f + b.R * kInvPi;
+    if (reflect) f = f + bxdf_f(b, wo, wi);
     return f;
 }
 

@@ -59,6 +59,14 @@ struct LinearNode {
 };
 static_assert(sizeof(LinearNode) == 32, "LinearBVHNode must be 32 bytes");
 
+// Shape "plymesh" file contents (ply.cpp).
+struct PlyMesh {
+    std::vector<float> P, N, UV;
+    std::vector<int> idx;
+    bool hasN = false, hasUV = false;
+};
+void read_ply(const std::string& path, PlyMesh* out);
+
 // SAH BVH build over the scene's primitives (bvh.cpp:190-402, 640-658).
 // prim_order[i] = index into desc->prims of the i-th primitive in BVH order.
 void build_bvh(const pt_scene_desc* d, std::vector<LinearNode>* nodes, std::vector<int>* prim_order);

@@ -834,8 +834,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
         }
         if (found && bounces < sc.max_depth) {
-            const pt_material m = sc.mats[mat];
-            if (m.kind == PT_MAT_NONE) {
+            if (sc.mats[mat].kind == PT_MAT_NONE) {
                 // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
                 const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
                 store_ray6(ps.ray, N, slot, r);
@@ -844,7 +843,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
             } else {
                 Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
                 Bsdf bsdf;
-                make_bsdf(m, si, &bsdf);
+                make_bsdf(&sc.mats[mat], si, &bsdf);
                 if (bsdf.nbxdf > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
                     bool deferred = false;
@@ -1089,6 +1088,33 @@ __global__ __launch_bounds__(kTraceBlock) void k_debug_trace(DevScene sc, const 
     int* sp = spill + (size_t)i * (64 - kStackLds);
     out_prim[i] = any ? traverse<true>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b)
                       : traverse<false>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b);
+}
+
+// BSDF of scene material `mat` in the local frame n = (0,0,1): for each i,
+// in[8i..]: wo(3), wi(3), u0, u1 -> out[8i..]: f(3), pdf, sampled wi(3), sampled pdf
+// (sampled f replaces f when in wi is all zero).
+__global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* a = in + 8 * i;
+    SurfHit si{};
+    si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
+    Bsdf b;
+    make_bsdf(&sc.mats[mat], si, &b);
+    const V3 wo = v3(a[0], a[1], a[2]), wi = v3(a[3], a[4], a[5]);
+    float* o = out + 8 * i;
+    S3 f = s3(0.f);
+    float pdf = 0;
+    if (wi.x != 0 || wi.y != 0 || wi.z != 0) {
+        f = bsdf_f(b, wo, wi);
+        pdf = bsdf_pdf(b, wo, wi);
+    }
+    V3 ws = v3(0, 0, 0);
+    float spdf = 0;
+    const S3 sf = bsdf_sample(b, wo, &ws, a[6], a[7], &spdf);
+    if (wi.x == 0 && wi.y == 0 && wi.z == 0) f = sf;
+    o[0] = f.c[0]; o[1] = f.c[1]; o[2] = f.c[2]; o[3] = pdf;
+    o[4] = ws.x; o[5] = ws.y; o[6] = ws.z; o[7] = spdf;
 }
 
 }  // namespace pt

@@ -339,6 +339,14 @@ struct ParamSet {
     }
 };
 
+// TrowbridgeReitzDistribution::RoughnessToAlpha (microfacet.h:127-132), float
+// arithmetic and the platform logf as the reference binary evaluates it.
+float tr_roughness_to_alpha(float roughness) {
+    roughness = std::max(roughness, (float)1e-3);
+    const float x = std::log(roughness);
+    return 1.62142f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
+}
+
 struct Directive {
     std::string name;
     ParamSet ps;
@@ -382,6 +390,7 @@ class Loader {
         ss << f.rdbuf();
         std::string dir = path.substr(0, path.find_last_of('/') == std::string::npos ? 0 : path.find_last_of('/') + 1);
         dirs_.push_back(dir);
+        if (dirs_.size() == 1) searchDir_ = dir;  // SetSearchDirectory (parser.cpp:1095)
         parse_text(ss.str());
         dirs_.pop_back();
     }
@@ -393,6 +402,7 @@ class Loader {
   private:
     pt_host_scene_impl* out_;
     std::vector<std::string> dirs_;
+    std::string searchDir_;
     HXF ctm_ = hxf_identity();
     std::vector<HXF> xfStack_;
     GraphicsState gs_;
@@ -576,7 +586,7 @@ class Loader {
                 shape(n, tmp.ps);
             } else if (d == "Include") {
                 std::string f = read_string(tk);
-                if (f.empty() || f[0] != '/') f = dirs_.back() + f;
+                if (f.empty() || f[0] != '/') f = searchDir_ + f;  // ResolveFilename (fileutil.cpp:105-114)
                 parse_file(f);
             } else if (d == "Texture" || d == "MakeNamedMedium" || d == "MediumInterface" || d == "ObjectBegin" ||
                        d == "ObjectEnd" || d == "ObjectInstance" || d == "TransformTimes" ||
@@ -607,11 +617,97 @@ class Loader {
             if (sigma != 0.f) throw PtError(PT_ERR_UNSUPPORTED, "OrenNayar (sigma != 0) is outside the supported subset");
             m.kd[0] = kd[0]; m.kd[1] = kd[1]; m.kd[2] = kd[2];
             m.sigma = sigma;
+        } else if (name == "metal") {
+            // CreateMetalMaterial (metal.cpp:113-131).  The default eta/k are
+            // copper spectra (Spectrum::FromSampled needs the CIE tables), so
+            // both must be given as rgb here.
+            m.kind = PT_MAT_METAL;
+            for (const char* tex : {"eta", "k", "roughness", "uroughness", "vroughness", "bumpmap"})
+                if (gs_.materialParams.find(tex, {"texture"}) || shapeParams.find(tex, {"texture"}))
+                    throw PtError(PT_ERR_UNSUPPORTED, "textured metal parameters are outside the supported subset");
+            float eta[3], k[3];
+            bool hasEta = gs_.materialParams.spectrum("eta", eta);
+            hasEta = shapeParams.spectrum("eta", eta) || hasEta;
+            bool hasK = gs_.materialParams.spectrum("k", k);
+            hasK = shapeParams.spectrum("k", k) || hasK;
+            if (!hasEta || !hasK)
+                throw PtError(PT_ERR_UNSUPPORTED, "metal needs rgb \"eta\" and \"k\" (the copper default is spectral)");
+            auto f1 = [&](const char* n, float def, bool* found) {
+                const Param* p = shapeParams.floats(n);
+                if (!p) p = gs_.materialParams.floats(n);
+                if (found) *found = p && !p->nums.empty();
+                return (p && !p->nums.empty()) ? (float)p->nums[0] : def;
+            };
+            const float rough = f1("roughness", .01f, nullptr);
+            bool hu = false, hv = false;
+            float ur = f1("uroughness", 0.f, &hu), vr = f1("vroughness", 0.f, &hv);
+            if (!hu) ur = rough;
+            if (!hv) vr = rough;
+            bool remap = gs_.materialParams.bool1("remaproughness", true);
+            remap = shapeParams.bool1("remaproughness", remap);
+            if (remap) {
+                ur = tr_roughness_to_alpha(ur);
+                vr = tr_roughness_to_alpha(vr);
+            }
+            for (int i = 0; i < 3; ++i) { m.eta[i] = eta[i]; m.k[i] = k[i]; }
+            m.alpha[0] = std::max(0.001f, ur);  // TrowbridgeReitzDistribution ctor (microfacet.h:109-113)
+            m.alpha[1] = std::max(0.001f, vr);
         } else {
             throw PtError(PT_ERR_UNSUPPORTED, "material \"" + name + "\" is outside the supported subset");
         }
         out_->materials.push_back(m);
         return (int)out_->materials.size() - 1;
+    }
+
+    // CreateTriangleMesh + TriangleMesh ctor (triangle.cpp:55-120): vertices,
+    // normals and tangents to world space, one Triangle (and one
+    // DiffuseAreaLight, api.cpp MakeShapes) per index triple.
+    void add_mesh(const ParamSet& ps, uint32_t oflags, const std::vector<float>& P, const std::vector<float>& Nv,
+                  const std::vector<float>& Sv, const std::vector<float>& UVv, const std::vector<int>& idx) {
+        const HXF o2w = ctm_;
+        const int nv = (int)P.size() / 3;
+        if (idx.size() % 3 != 0) throw PtError(PT_ERR_PARSE, "indices not a multiple of 3");
+        for (int v : idx)
+            if (v < 0 || v >= nv) throw PtError(PT_ERR_PARSE, "trianglemesh index out of range");
+        const bool hasN = (int)Nv.size() == 3 * nv, hasS = (int)Sv.size() == 3 * nv, hasUV = (int)UVv.size() == 2 * nv;
+        const int base = (int)out_->P.size() / 3;
+        for (int i = 0; i < nv; ++i) {
+            V3 w = xf_point(to_m4(o2w.m), v3(P[3 * i], P[3 * i + 1], P[3 * i + 2]));  // triangle.cpp:75
+            out_->P.push_back(w.x); out_->P.push_back(w.y); out_->P.push_back(w.z);
+            V3 n = v3(0, 0, 0), s = v3(0, 0, 0);
+            if (hasN) n = xf_normal(to_m4(o2w.mi), v3(Nv[3 * i], Nv[3 * i + 1], Nv[3 * i + 2]));
+            if (hasS) s = xf_vector(to_m4(o2w.m), v3(Sv[3 * i], Sv[3 * i + 1], Sv[3 * i + 2]));
+            out_->N.push_back(n.x); out_->N.push_back(n.y); out_->N.push_back(n.z);
+            out_->S.push_back(s.x); out_->S.push_back(s.y); out_->S.push_back(s.z);
+            out_->UV.push_back(hasUV ? UVv[2 * i] : 0.f);
+            out_->UV.push_back(hasUV ? UVv[2 * i + 1] : 0.f);
+        }
+        out_->anyN |= hasN; out_->anyS |= hasS; out_->anyUV |= hasUV;
+        const int mat = material_for(ps);
+        const uint32_t flags =
+            oflags | (hasN ? PT_TRI_HAS_N : 0u) | (hasS ? PT_TRI_HAS_S : 0u) | (hasUV ? PT_TRI_HAS_UV : 0u);
+        const int ntri = (int)idx.size() / 3;
+        for (int t = 0; t < ntri; ++t) {
+            pt_triangle tr{};
+            tr.v[0] = base + idx[3 * t]; tr.v[1] = base + idx[3 * t + 1]; tr.v[2] = base + idx[3 * t + 2];
+            tr.material = mat;
+            tr.area_light = -1;
+            tr.flags = flags;
+            const int ti = (int)out_->tris.size();
+            if (!gs_.areaLight.empty()) {
+                if (gs_.areaLight != "diffuse" && gs_.areaLight != "area")
+                    throw PtError(PT_ERR_UNSUPPORTED, "area light \"" + gs_.areaLight + "\" on a triangle mesh");
+                pt_light L{};
+                L.kind = PT_LIGHT_DIFFUSE_AREA;
+                diffuse_params(gs_.areaLightParams, &L);
+                L.shape = ti;
+                L.first_portal = 0; L.n_portals = 0;
+                out_->lights.push_back(L);
+                tr.area_light = (int)out_->lights.size() - 1;
+            }
+            out_->tris.push_back(tr);
+            out_->prims.push_back(pt_prim{PT_PRIM_TRIANGLE, ti});
+        }
     }
 
     void shape(const std::string& name, const ParamSet& ps) {
@@ -620,67 +716,40 @@ class Loader {
         const bool ro = gs_.reverseOrientation;
         const bool sh = hxf_swaps_handedness(o2w);
         uint32_t oflags = (ro ? PT_TRI_REVERSE_ORIENTATION : 0u) | (sh ? PT_TRI_SWAPS_HANDEDNESS : 0u);
-        if (name == "trianglemesh") {
-            const Param* pi = ps.find("indices", {"integer"});
-            const Param* pp = ps.find("P", {"point"});
-            if (!pp || pp->nums.size() % 3 != 0 || pp->nums.empty())
-                throw PtError(PT_ERR_PARSE, "trianglemesh needs \"point P\"");
-            int nv = (int)pp->nums.size() / 3;
-            std::vector<int> idx;
-            if (pi) for (double v : pi->nums) idx.push_back(int(v));
-            else if (nv == 3) idx = {0, 1, 2};
-            else throw PtError(PT_ERR_PARSE, "trianglemesh needs \"integer indices\"");
-            if (idx.size() % 3 != 0) throw PtError(PT_ERR_PARSE, "indices not a multiple of 3");
-            for (int v : idx)
-                if (v < 0 || v >= nv) throw PtError(PT_ERR_PARSE, "trianglemesh index out of range");
-            const Param* pn = ps.find("N", {"normal"});
-            const Param* pS = ps.find("S", {"vector"});
-            const Param* puv = ps.find("uv", {"point2", "float"});
-            if (!puv) puv = ps.find("st", {"point2", "float"});
+        if (name == "trianglemesh" || name == "plymesh") {
             if (ps.find("alpha", {"texture", "float"}) || ps.find("shadowalpha", {"texture", "float"}))
                 throw PtError(PT_ERR_UNSUPPORTED, "alpha textures are outside the supported subset");
-            bool hasN = pn && (int)pn->nums.size() == 3 * nv;
-            bool hasS = pS && (int)pS->nums.size() == 3 * nv;
-            bool hasUV = puv && (int)puv->nums.size() == 2 * nv;
-            int base = (int)out_->P.size() / 3;
-            for (int i = 0; i < nv; ++i) {
-                V3 p = v3((float)pp->nums[3 * i], (float)pp->nums[3 * i + 1], (float)pp->nums[3 * i + 2]);
-                V3 w = xf_point(to_m4(o2w.m), p);  // TriangleMesh ctor (triangle.cpp:75)
-                out_->P.push_back(w.x); out_->P.push_back(w.y); out_->P.push_back(w.z);
-                V3 n = v3(0, 0, 0), s = v3(0, 0, 0);
-                if (hasN) n = xf_normal(to_m4(o2w.mi), v3((float)pn->nums[3 * i], (float)pn->nums[3 * i + 1], (float)pn->nums[3 * i + 2]));
-                if (hasS) s = xf_vector(to_m4(o2w.m), v3((float)pS->nums[3 * i], (float)pS->nums[3 * i + 1], (float)pS->nums[3 * i + 2]));
-                out_->N.push_back(n.x); out_->N.push_back(n.y); out_->N.push_back(n.z);
-                out_->S.push_back(s.x); out_->S.push_back(s.y); out_->S.push_back(s.z);
-                out_->UV.push_back(hasUV ? (float)puv->nums[2 * i] : 0.f);
-                out_->UV.push_back(hasUV ? (float)puv->nums[2 * i + 1] : 0.f);
+            std::vector<float> P, N, S, UV;
+            std::vector<int> idx;
+            if (name == "trianglemesh") {
+                const Param* pi = ps.find("indices", {"integer"});
+                const Param* pp = ps.find("P", {"point"});
+                if (!pp || pp->nums.size() % 3 != 0 || pp->nums.empty())
+                    throw PtError(PT_ERR_PARSE, "trianglemesh needs \"point P\"");
+                const int nv = (int)pp->nums.size() / 3;
+                if (pi) for (double v : pi->nums) idx.push_back(int(v));
+                else if (nv == 3) idx = {0, 1, 2};
+                else throw PtError(PT_ERR_PARSE, "trianglemesh needs \"integer indices\"");
+                const Param* pn = ps.find("N", {"normal"});
+                const Param* pS = ps.find("S", {"vector"});
+                const Param* puv = ps.find("uv", {"point2", "float"});
+                if (!puv) puv = ps.find("st", {"point2", "float"});
+                for (double v : pp->nums) P.push_back((float)v);
+                if (pn && (int)pn->nums.size() == 3 * nv) for (double v : pn->nums) N.push_back((float)v);
+                if (pS && (int)pS->nums.size() == 3 * nv) for (double v : pS->nums) S.push_back((float)v);
+                if (puv && (int)puv->nums.size() == 2 * nv) for (double v : puv->nums) UV.push_back((float)v);
+            } else {
+                // CreatePLYMesh (plymesh.cpp:107-235); filename relative to the search directory
+                std::string f = ps.string1("filename", "");
+                if (!f.empty() && f[0] != '/') f = searchDir_ + f;
+                PlyMesh m;
+                read_ply(f, &m);
+                P = std::move(m.P);
+                N = std::move(m.N);
+                UV = std::move(m.UV);
+                idx = std::move(m.idx);
             }
-            out_->anyN |= hasN; out_->anyS |= hasS; out_->anyUV |= hasUV;
-            int mat = material_for(ps);
-            uint32_t flags = oflags | (hasN ? PT_TRI_HAS_N : 0u) | (hasS ? PT_TRI_HAS_S : 0u) | (hasUV ? PT_TRI_HAS_UV : 0u);
-            int ntri = (int)idx.size() / 3;
-            std::vector<int> newLights;
-            for (int t = 0; t < ntri; ++t) {
-                pt_triangle tr{};
-                tr.v[0] = base + idx[3 * t]; tr.v[1] = base + idx[3 * t + 1]; tr.v[2] = base + idx[3 * t + 2];
-                tr.material = mat;
-                tr.area_light = -1;
-                tr.flags = flags;
-                int ti = (int)out_->tris.size();
-                if (!gs_.areaLight.empty()) {
-                    if (gs_.areaLight != "diffuse" && gs_.areaLight != "area")
-                        throw PtError(PT_ERR_UNSUPPORTED, "area light \"" + gs_.areaLight + "\" on a trianglemesh");
-                    pt_light L{};
-                    L.kind = PT_LIGHT_DIFFUSE_AREA;
-                    diffuse_params(gs_.areaLightParams, &L);
-                    L.shape = ti;
-                    L.first_portal = 0; L.n_portals = 0;
-                    out_->lights.push_back(L);
-                    tr.area_light = (int)out_->lights.size() - 1;
-                }
-                out_->tris.push_back(tr);
-                out_->prims.push_back(pt_prim{PT_PRIM_TRIANGLE, ti});
-            }
+            add_mesh(ps, oflags, P, N, S, UV, idx);
         } else if (name == "aaplane") {
             // CreateAAPlaneShape (plane.cpp:117-128)
             V3 lo = v3(0, 0, 0), hi = v3(0, 0, 0);

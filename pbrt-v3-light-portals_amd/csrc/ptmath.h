@@ -98,6 +98,9 @@ PTHD S3 s3(float a, float b, float c) { return S3{{a, b, c}}; }
 PTHD S3 operator*(S3 a, S3 b) { return s3(a.c[0] * b.c[0], a.c[1] * b.c[1], a.c[2] * b.c[2]); }
 PTHD S3 operator*(S3 a, float f) { return s3(a.c[0] * f, a.c[1] * f, a.c[2] * f); }
 PTHD S3 operator/(S3 a, float f) { return s3(a.c[0] / f, a.c[1] / f, a.c[2] / f); }
+PTHD S3 operator/(S3 a, S3 b) { return s3(a.c[0] / b.c[0], a.c[1] / b.c[1], a.c[2] / b.c[2]); }
+PTHD S3 operator-(S3 a, S3 b) { return s3(a.c[0] - b.c[0], a.c[1] - b.c[1], a.c[2] - b.c[2]); }
+PTHD S3 ssqrt(S3 a) { return s3(sqrtf(a.c[0]), sqrtf(a.c[1]), sqrtf(a.c[2])); }  // Sqrt(Spectrum)
 PTHD S3 operator+(S3 a, S3 b) { return s3(a.c[0] + b.c[0], a.c[1] + b.c[1], a.c[2] + b.c[2]); }
 PTHD bool is_black(S3 a) { return a.c[0] == 0.f && a.c[1] == 0.f && a.c[2] == 0.f; }
 PTHD float max_comp(S3 a) { float m = a.c[0]; m = smax(m, a.c[1]); m = smax(m, a.c[2]); return m; }
@@ -298,6 +301,61 @@ PTHD int find_interval(const float* cdf, int size, float u) {
     int r = first - 1;
     r = r < 0 ? 0 : r;
     return r > size - 2 ? size - 2 : r;
+}
+
+// ---- double-precision sin/cos for moderate arguments ---------------------------
+// The reference calls <math.h>'s double cos/sin in TrowbridgeReitzSample11
+// (phi in [0, 2pi)).  These follow the classic fdlibm kernels (k_sin.c,
+// k_cos.c) after a two-constant pi/2 reduction: < 1 ulp in double, so the
+// float results the reference derives from them agree with glibc except when
+// a double lands within 1 ulp of a float rounding boundary (~2^-28 odds).
+// Valid for |x| < 2^19 * pi/2.
+constexpr double kDS1 = -1.66666666666666324348e-01, kDS2 = 8.33333333332248946124e-03,
+                 kDS3 = -1.98412698298579493134e-04, kDS4 = 2.75573137070700676789e-06,
+                 kDS5 = -2.50507602534068634195e-08, kDS6 = 1.58969099521155010221e-10;
+constexpr double kDC1 = 4.16666666666666019037e-02, kDC2 = -1.38888888888741095749e-03,
+                 kDC3 = 2.48015872894767294178e-05, kDC4 = -2.75573143513906633035e-07,
+                 kDC5 = 2.08757232129817482790e-09, kDC6 = -1.13596475577881948265e-11;
+constexpr double kPio2_1 = 1.57079632673412561417e+00, kPio2_1t = 6.07710050650619224932e-11;
+constexpr double kInvPio2 = 6.36619772367581382433e-01;
+PTHD double dk_sin(double x, double y) {
+    const double z = x * x, v = z * x;
+    const double r = kDS2 + z * (kDS3 + z * (kDS4 + z * (kDS5 + z * kDS6)));
+    return x - ((z * (0.5 * y - v * r) - y) - v * kDS1);
+}
+PTHD double dk_cos(double x, double y) {
+    const double z = x * x;
+    const double r = z * (kDC1 + z * (kDC2 + z * (kDC3 + z * (kDC4 + z * (kDC5 + z * kDC6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+PTHD void dsincos_reduce(double x, int* q, double* hi, double* lo) {
+    const double n = __builtin_rint(x * kInvPio2);
+    const double r = x - n * kPio2_1;
+    const double w = n * kPio2_1t;
+    *hi = r - w;
+    *lo = (r - *hi) - w;
+    *q = (int)n & 3;
+}
+PTHD double dsin_mod(double x) {
+    int q; double a, b;
+    dsincos_reduce(x, &q, &a, &b);
+    switch (q) {
+        case 0: return dk_sin(a, b);
+        case 1: return dk_cos(a, b);
+        case 2: return -dk_sin(a, b);
+        default: return -dk_cos(a, b);
+    }
+}
+PTHD double dcos_mod(double x) {
+    int q; double a, b;
+    dsincos_reduce(x, &q, &a, &b);
+    switch (q) {
+        case 0: return dk_cos(a, b);
+        case 1: return -dk_sin(a, b);
+        case 2: return -dk_cos(a, b);
+        default: return dk_sin(a, b);
+    }
 }
 
 // ---- low discrepancy (core/lowdiscrepancy.{h,cpp}) ----------------------------

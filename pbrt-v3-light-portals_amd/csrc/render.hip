@@ -1086,4 +1086,18 @@ pt_status pt_debug_trace(pt_scene* s, int n, const float* rays7, int any, int32_
     });
 }
 
+pt_status pt_debug_bsdf(pt_scene* s, int material, int n, const float* in8, float* out8) {
+    return guarded([&] {
+        if (!s || n < 0 || (n && (!in8 || !out8))) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        if (material < 0 || material >= (int)s->mats.n) throw PtError(PT_ERR_INVALID_ARG, "material out of range");
+        if (n == 0) return;
+        DBuf<float> di, dout;
+        di.upload(in8, (size_t)8 * n);
+        dout.alloc((size_t)8 * n);
+        hipLaunchKernelGGL(k_debug_bsdf, dim3(ceil_div(n, 128)), dim3(128), 0, 0, s->dev, material, di.p, n, dout.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpy(out8, dout.p, sizeof(float) * 8 * n, hipMemcpyDeviceToHost));
+    });
+}
+
 }  // extern "C"

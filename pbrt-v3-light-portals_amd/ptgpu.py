@@ -85,6 +85,7 @@ def lib() -> ctypes.CDLL:
     L.pt_debug_pixel_offsets.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_camera_rays.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_trace.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
+    L.pt_debug_bsdf.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     _lib = L
     return L
 
@@ -96,6 +97,21 @@ def _check(status: int) -> None:
 
 def _fptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class pt_material(ctypes.Structure):
+    """include/pt.h pt_material"""
+    _fields_ = [("kind", ctypes.c_int32), ("kd", ctypes.c_float * 3), ("sigma", ctypes.c_float),
+                ("eta", ctypes.c_float * 3), ("k", ctypes.c_float * 3), ("alpha", ctypes.c_float * 2)]
+
+
+class _desc_prefix(ctypes.Structure):
+    """Leading fields of include/pt.h pt_scene_desc (through the materials)."""
+    _fields_ = [("n_vertices", ctypes.c_int32), ("P", ctypes.c_void_p), ("N", ctypes.c_void_p),
+                ("S", ctypes.c_void_p), ("UV", ctypes.c_void_p), ("n_triangles", ctypes.c_int32),
+                ("triangles", ctypes.c_void_p), ("n_planes", ctypes.c_int32), ("planes", ctypes.c_void_p),
+                ("n_prims", ctypes.c_int32), ("prims", ctypes.c_void_p), ("n_materials", ctypes.c_int32),
+                ("materials", ctypes.POINTER(pt_material))]
 
 
 class HostScene:
@@ -121,6 +137,11 @@ class HostScene:
         _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), nodes.ctypes.data, order.ctypes.data,
                                        int(2 * n.value)))
         return nodes, order
+
+    def materials(self) -> list:
+        """The scene's pt_material records (copies) -- host only."""
+        d = ctypes.cast(ctypes.c_void_p(self.desc), ctypes.POINTER(_desc_prefix)).contents
+        return [pt_material.from_buffer_copy(d.materials[i]) for i in range(d.n_materials)]
 
     def film_size(self) -> Tuple[int, int]:
         """Cropped film (width, height) -- host only."""
@@ -247,6 +268,13 @@ class Scene:
         rays7 = np.ascontiguousarray(rays7, np.float32)
         out = np.zeros(len(rays7), np.int32)
         _check(lib().pt_debug_trace(self._s, len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data))
+        return out
+
+    def debug_bsdf(self, material: int, rec8: np.ndarray) -> np.ndarray:
+        """(n, 8) records wo, wi, u0, u1 -> (n, 8) f, pdf, sampled wi, sampled pdf."""
+        rec8 = np.ascontiguousarray(rec8, np.float32)
+        out = np.zeros_like(rec8)
+        _check(lib().pt_debug_bsdf(self._s, material, len(rec8), rec8.ctypes.data, out.ctypes.data))
         return out
 
     def close(self) -> None:

@@ -201,3 +201,53 @@ def test_trace_variants_bit_exact(variant, monkeypatch, env):
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst["node_visits"] == rst["node_visits"]
+
+
+def _bsdf_records(n, seed):
+    rng = np.random.default_rng(seed)
+    wo = rng.normal(size=(n, 3))
+    wo[: n // 8] = [1e-3, -2e-3, 1.0]               # normal incidence: TrowbridgeReitzSample11's double branch
+    wo[n // 8: n // 4, 2] = np.abs(wo[n // 8: n // 4, 2]) * 50
+    wo /= np.linalg.norm(wo, axis=1, keepdims=True)
+    wi = rng.normal(size=(n, 3))
+    wi /= np.linalg.norm(wi, axis=1, keepdims=True)
+    wi[::5] = 0                                      # sample-only records
+    u = rng.random((n, 2)) * 0.99999994
+    return np.concatenate([wo, wi, u], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("rough", ['"float roughness" [0.3]', '"float uroughness" [0.0] "float vroughness" [0.0]',
+                                   '"float uroughness" [0.6] "float vroughness" [0.05]'])
+def test_metal_bsdf_bit_exact(tmp_path, rough):
+    """BSDF::f / Pdf / Sample_f of MetalMaterial (TrowbridgeReitz visible-normal
+    sampling, FresnelConductor) and of the matte materials: device == oracle."""
+    from test_materials import _metal_index, metal_scene
+    hs, sc = _scene(metal_scene(tmp_path, rough=rough, **MINI))
+    rec = _bsdf_records(20000, 11)
+    for mat in range(len(hs.materials())):
+        got = sc.debug_bsdf(mat, rec)
+        ref = pyoracle.bsdf_batch(hs.desc, mat, rec)
+        bad = np.nonzero(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=1))[0]
+        assert len(bad) == 0, (mat, bad[:5], got[bad[:3]], ref[bad[:3]])
+    assert _metal_index(hs) >= 0
+
+
+@pytest.mark.parametrize("strategy", ["portal", "projection"])
+def test_metal_render_matches_oracle(tmp_path, strategy):
+    from test_materials import metal_scene
+    hs, sc = _scene(metal_scene(tmp_path, rough='"float uroughness" [0.05] "float vroughness" [0.2]',
+                                strategy=strategy, **MINI))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst["closest_rays"] == rst["closest_rays"]
+
+
+def test_plymesh_metal_render_matches_oracle(tmp_path):
+    from test_materials import ply_scene
+    hs, sc = _scene(ply_scene(tmp_path, material='Material "metal" "rgb eta" [0.8 0.8 0.8] "rgb k" [0.8 0.8 0.8] '
+                                                 '"float roughness" [0.1]', **MINI))
+    ref, _ = pyoracle.render(hs.desc, nthreads=8)
+    got, _ = sc.render()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -1,0 +1,235 @@
+"""Materials beyond matte: MetalMaterial (materials/metal.cpp) =
+MicrofacetReflection + TrowbridgeReitz + FresnelConductor.
+
+CPU: the loader's parameter handling (RoughnessToAlpha, defaults, errors) and
+the oracle's microfacet sampling restated from the reference's own
+BSDFSampling chi^2 tests (src/tests/bsdfs.cpp:173-438, TR_VA_* cases)."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+import ptgpu
+import pyoracle
+from conftest import scene_variant
+
+F32 = np.float32
+
+
+def _logf(x):
+    libm = ctypes.CDLL("libm.so.6")
+    libm.logf.restype = ctypes.c_float
+    libm.logf.argtypes = [ctypes.c_float]
+    return F32(libm.logf(F32(x)))
+
+
+def roughness_to_alpha(r):
+    """microfacet.h:127-132 in float arithmetic"""
+    r = max(F32(r), F32(1e-3))
+    x = _logf(r)
+    return F32(F32(F32(F32(F32(1.62142) + F32(F32(0.819955) * x)) + F32(F32(F32(0.1734) * x) * x))
+                   + F32(F32(F32(F32(0.0171201) * x) * x) * x))
+               + F32(F32(F32(F32(F32(0.000640711) * x) * x) * x) * x))
+
+
+METAL_BOX = '''
+AttributeBegin
+  Material "metal" "rgb eta" [0.2 0.9 1.1] "rgb k" [3.9 2.4 2.2] {rough}
+  Shape "trianglemesh" "point P" [150 0 150  400 0 150  400 200 300  150 200 300] "integer indices" [0 1 2 0 2 3]
+AttributeEnd
+'''
+
+
+def metal_scene(tmp_path, rough='"float roughness" [0.3]', **kw):
+    return scene_variant(tmp_path, extra=[("WorldEnd", METAL_BOX.format(rough=rough) + "WorldEnd")], **kw)
+
+
+def _metal_index(hs):
+    mats = hs.materials()
+    idx = [i for i, m in enumerate(mats) if m.kind == 2]
+    assert idx, "no metal material"
+    return idx[0]
+
+
+@pytest.mark.parametrize("rough,expect", [('"float roughness" [0.3]', (0.3, 0.3)),
+                                          ('"float uroughness" [0.5] "float vroughness" [0.1]', (0.5, 0.1)),
+                                          ('"float roughness" [0.2] "float uroughness" [0.0]', (0.0, 0.2)),
+                                          ('', (0.01, 0.01))])
+def test_metal_roughness_to_alpha(tmp_path, rough, expect):
+    hs = ptgpu.HostScene(metal_scene(tmp_path, rough=rough, res=(8, 8), spp=1))
+    m = hs.materials()[_metal_index(hs)]
+    for got, r in zip(m.alpha, expect):
+        assert F32(got) == max(F32(0.001), roughness_to_alpha(r))
+    assert list(m.eta) == [F32(0.2), F32(0.9), F32(1.1)]
+
+
+def test_metal_no_remap(tmp_path):
+    hs = ptgpu.HostScene(metal_scene(tmp_path, rough='"float roughness" [0.25] "bool remaproughness" "false"',
+                                     res=(8, 8), spp=1))
+    m = hs.materials()[_metal_index(hs)]
+    assert list(m.alpha) == [F32(0.25), F32(0.25)]
+
+
+def test_metal_default_copper_is_refused(tmp_path):
+    p = scene_variant(tmp_path, extra=[("WorldEnd", 'Material "metal"\nShape "trianglemesh" "point P" '
+                                                    '[0 0 0 1 0 0 1 1 0] "integer indices" [0 1 2]\nWorldEnd')])
+    with pytest.raises(ptgpu.PtError) as e:
+        ptgpu.HostScene(p)
+    assert e.value.status == 3  # PT_ERR_UNSUPPORTED
+
+
+def _cosine_hemisphere(u0, u1):
+    # CosineSampleHemisphere(ConcentricSampleDisk) is only used to pick wo here
+    r = math.sqrt(u0)
+    phi = 2 * math.pi * u1
+    return np.array([r * math.cos(phi), r * math.sin(phi), math.sqrt(max(0.0, 1 - u0))])
+
+
+@pytest.mark.parametrize("rough", ['"float roughness" [0.5] "bool remaproughness" "false"',
+                                   '"float uroughness" [0.3] "float vroughness" [0.15] "bool remaproughness" "false"',
+                                   '"float roughness" [0.3] "bool remaproughness" "false"'])
+def test_microfacet_sampling_chi2(tmp_path, rough):
+    """BSDFSampling.TR_VA_0p5 / TR_VA_0p3_0p15 / TR_VA_0p3 (bsdfs.cpp:493-546):
+    histogram of Sample_f directions vs N * integral of Pdf per (theta, phi)
+    cell, chi^2 with low-frequency cells merged (CHI2_MINFREQ 5), significance
+    0.01 Bonferroni-corrected over the runs."""
+    from scipy.stats import chi2
+    hs = ptgpu.HostScene(metal_scene(tmp_path, rough=rough, res=(8, 8), spp=1))
+    mat = _metal_index(hs)
+    rng = np.random.default_rng(7)
+    theta_res, phi_res, n, runs = 10, 20, 400000, 3
+    sig = 1.0 - (1.0 - 0.01) ** (1.0 / runs)
+    for run in range(runs):
+        wo = _cosine_hemisphere(*rng.random(2)).astype(np.float32)
+        rec = np.zeros((n, 8), np.float32)
+        rec[:, 0:3] = wo
+        rec[:, 6:8] = rng.random((n, 2), dtype=np.float32) * F32(0.99999994)
+        out = pyoracle.bsdf_batch(hs.desc, mat, rec)
+        ok = (out[:, 0:3].max(axis=1) > 0) & (out[:, 7] > 0)
+        wi = out[ok, 4:7].astype(np.float64)
+        th = np.arccos(np.clip(wi[:, 2], -1, 1)) * theta_res / math.pi
+        ph = np.arctan2(wi[:, 1], wi[:, 0])
+        ph = np.where(ph < 0, ph + 2 * math.pi, ph) * phi_res / (2 * math.pi)
+        ti = np.clip(np.floor(th).astype(int), 0, theta_res - 1)
+        pi_ = np.clip(np.floor(ph).astype(int), 0, phi_res - 1)
+        obs = np.bincount(ti * phi_res + pi_, minlength=theta_res * phi_res).astype(np.float64)
+        # expected: midpoint rule, 12 x 12 points per cell, pdf * sin(theta)
+        k = 12
+        tt = (np.arange(theta_res * k) + 0.5) * math.pi / (theta_res * k)
+        pp = (np.arange(phi_res * k) + 0.5) * 2 * math.pi / (phi_res * k)
+        T, P = np.meshgrid(tt, pp, indexing="ij")
+        dirs = np.stack([np.sin(T) * np.cos(P), np.sin(T) * np.sin(P), np.cos(T)], -1).reshape(-1, 3)
+        q = np.zeros((len(dirs), 8), np.float32)
+        q[:, 0:3] = wo
+        q[:, 3:6] = dirs
+        pdf = pyoracle.bsdf_batch(hs.desc, mat, q)[:, 3].astype(np.float64).reshape(theta_res * k, phi_res * k)
+        cell = (math.pi / (theta_res * k)) * (2 * math.pi / (phi_res * k))
+        dens = pdf * np.sin(T) * cell
+        exp = dens.reshape(theta_res, k, phi_res, k).sum(axis=(1, 3)).reshape(-1) * n
+        # merge cells with expected frequency < 5 (bsdfs.cpp Chi2Test)
+        order = np.argsort(exp)
+        stat, dof, pool_o, pool_e = 0.0, 0, 0.0, 0.0
+        for i in order:
+            if exp[i] < 5:
+                pool_o += obs[i]
+                pool_e += exp[i]
+                continue
+            stat += (obs[i] - exp[i]) ** 2 / exp[i]
+            dof += 1
+        if pool_e >= 5:
+            stat += (pool_o - pool_e) ** 2 / pool_e
+            dof += 1
+        pval = 1.0 - chi2.cdf(stat, dof - 1)
+        assert pval > sig, (run, stat, dof, pval)
+
+
+# ---- PLY meshes (shapes/plymesh.cpp) ---------------------------------------------------------
+
+def _sphere_mesh(n=12, r=60.0, c=(280.0, 120.0, 300.0)):
+    verts, uvs, norms = [], [], []
+    for i in range(n + 1):
+        th = math.pi * i / n
+        for j in range(2 * n):
+            ph = 2 * math.pi * j / (2 * n)
+            d = (math.sin(th) * math.cos(ph), math.cos(th), math.sin(th) * math.sin(ph))
+            verts.append([c[0] + r * d[0], c[1] + r * d[1], c[2] + r * d[2]])
+            norms.append(d)
+            uvs.append([j / (2 * n), i / n])
+    faces = []
+    for i in range(n):
+        for j in range(2 * n):
+            a, b = i * 2 * n + j, i * 2 * n + (j + 1) % (2 * n)
+            c2, d2 = a + 2 * n, b + 2 * n
+            faces.append([a, b, d2, c2])          # quads: split (0,1,2),(3,0,2)
+    faces.append([0, 1, 2])                       # one triangle
+    faces.append([0, 1, 2, 3, 4])                 # a pentagon: skipped with a warning
+    return np.array(verts, np.float32), np.array(norms, np.float32), np.array(uvs, np.float32), faces
+
+
+def write_ply(path, verts, norms, uvs, faces, fmt="binary_little_endian", uvnames=("u", "v")):
+    head = ["ply", f"format {fmt} 1.0", "comment written by tests/test_materials.py", f"element vertex {len(verts)}",
+            "property float x", "property float y", "property float z", "property float nx", "property float ny",
+            "property float nz", f"property float {uvnames[0]}", f"property float {uvnames[1]}",
+            f"element face {len(faces)}", "property list uchar int vertex_indices", "end_header"]
+    with open(path, "wb") as f:
+        f.write(("\n".join(head) + "\n").encode())
+        if fmt == "ascii":
+            for v, nn, t in zip(verts, norms, uvs):
+                f.write((" ".join(repr(float(x)) for x in (*v, *nn, *t)) + "\n").encode())
+            for fc in faces:
+                f.write((" ".join(map(str, [len(fc), *fc])) + "\n").encode())
+        else:
+            e = "<" if fmt == "binary_little_endian" else ">"
+            import struct
+            for v, nn, t in zip(verts, norms, uvs):
+                f.write(struct.pack(e + "8f", *v, *nn, *t))
+            for fc in faces:
+                f.write(struct.pack(e + "B%di" % len(fc), len(fc), *fc))
+
+
+def ply_scene(tmp_path, fmt="binary_little_endian", material='Material "matte" "rgb Kd" [0.3 0.5 0.7]',
+              uvnames=("u", "v"), **kw):
+    v, nn, t, faces = _sphere_mesh()
+    write_ply(str(tmp_path / "ball.ply"), v, nn, t, faces, fmt=fmt, uvnames=uvnames)
+    extra = f'AttributeBegin\n  {material}\n  Shape "plymesh" "string filename" ["ball.ply"]\nAttributeEnd\nWorldEnd'
+    return scene_variant(tmp_path, extra=[("WorldEnd", extra)], **kw)
+
+
+def _trimesh_scene(tmp_path, **kw):
+    v, nn, t, faces = _sphere_mesh()
+    idx = []
+    for fc in faces:
+        if len(fc) == 3:
+            idx += fc
+        elif len(fc) == 4:
+            idx += [fc[0], fc[1], fc[2], fc[3], fc[0], fc[2]]
+    shape = ('Shape "trianglemesh" "integer indices" [%s] "point P" [%s] "normal N" [%s] "float uv" [%s]' %
+             (" ".join(map(str, idx)), " ".join(repr(float(x)) for x in v.reshape(-1)),
+              " ".join(repr(float(x)) for x in nn.reshape(-1)), " ".join(repr(float(x)) for x in t.reshape(-1))))
+    extra = f'AttributeBegin\n  Material "matte" "rgb Kd" [0.3 0.5 0.7]\n  {shape}\nAttributeEnd\nWorldEnd'
+    return scene_variant(tmp_path, extra=[("WorldEnd", extra)], **kw)
+
+
+@pytest.mark.parametrize("fmt,uvnames", [("binary_little_endian", ("u", "v")), ("binary_big_endian", ("s", "t")),
+                                         ("ascii", ("texture_u", "texture_v"))])
+def test_plymesh_equals_trianglemesh(tmp_path, fmt, uvnames):
+    """CreatePLYMesh feeds CreateTriangleMesh: the same mesh as a PLY file
+    (any encoding, quads split (0,1,2)+(3,0,2), non-tri/quad faces skipped)
+    renders bit-identically to the equivalent trianglemesh."""
+    a = ptgpu.HostScene(ply_scene(tmp_path, fmt=fmt, uvnames=uvnames, res=(24, 16), spp=2))
+    (tmp_path / "tri").mkdir()
+    b = ptgpu.HostScene(_trimesh_scene(tmp_path / "tri", res=(24, 16), spp=2))
+    ia, sa = pyoracle.render(a.desc, nthreads=4)
+    ib, sb = pyoracle.render(b.desc, nthreads=4)
+    assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32))
+    assert sa == sb
+
+
+def test_plymesh_bad_index_is_an_error(tmp_path):
+    v, nn, t, _ = _sphere_mesh()
+    write_ply(str(tmp_path / "ball.ply"), v, nn, t, [[0, 1, len(v) + 5]])
+    extra = 'Shape "plymesh" "string filename" ["ball.ply"]\nWorldEnd'
+    with pytest.raises(ptgpu.PtError) as e:
+        ptgpu.HostScene(scene_variant(tmp_path, extra=[("WorldEnd", extra)]))
+    assert e.value.status == 2  # PT_ERR_PARSE
