@@ -64,7 +64,8 @@ enum pt_material_kind {
 
 enum pt_light_kind {
     PT_LIGHT_DIFFUSE_AREA = 0, /* DiffuseAreaLight on one triangle   src/lights/diffuse.cpp */
-    PT_LIGHT_PORTAL_AREA = 1   /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
+    PT_LIGHT_PORTAL_AREA = 1,  /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
+    PT_LIGHT_INFINITE = 2      /* InfiniteAreaLight, constant L (no "mapname")  src/lights/infinite.cpp */
 };
 
 enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:12 */
@@ -142,6 +143,8 @@ typedef struct pt_light {
     int32_t strategy;     /* pt_portal_strategy (portal lights) */
     int32_t first_portal; /* into portals */
     int32_t n_portals;
+    int32_t n_samples;    /* Light::nSamples ("nsamples"/"samples", >= 1) */
+    pt_transform light_to_world; /* infinite: LightToWorld (CTM at the LightSource) */
 } pt_light;
 
 typedef struct pt_camera_desc {

@@ -376,6 +376,7 @@ typedef struct {
     float* ldist_cdf;
     float ldist_int;
     int nlights;
+    struct Inf* inf;           /* per light: InfiniteAreaLight data (kind INFINITE) */
     /* camera */
     M4 raster_to_camera;
     M4 camera_to_world;
@@ -1355,10 +1356,133 @@ static int si_material(const Scene* sc, const SI* si) {
     return kind == PT_PRIM_TRIANGLE ? sc->d->triangles[idx].material : sc->d->planes[idx].material;
 }
 
+/* ------------------------------------------------------------------------ */
+/* InfiniteAreaLight with a constant 1x1 Lmap (lights/infinite.cpp:43-132)    */
+/* ------------------------------------------------------------------------ */
+typedef struct Inf {
+    RGB L;                      /* the Lmap texel: L * scale */
+    XF l2w;                     /* LightToWorld (WorldToLight = its inverse) */
+    V3 center;                  /* Preprocess: WorldBound().BoundingSphere */
+    float radius;
+    /* Distribution2D over the 2x2 sinTheta-weighted luminance image */
+    float cfunc[2][2], ccdf[2][3], cint[2];
+    float mfunc[2], mcdf[3], mint;
+} Inf;
+
+/* MIPMap::triangle at level 0 of a 1x1 map with ImageWrap::Repeat (mipmap.h:264-274) */
+static RGB lmap_triangle(RGB v, float st0, float st1) {
+    float s = st0 * 1 - 0.5f, t = st1 * 1 - 0.5f;
+    int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    float ds = s - s0, dt = t - t0;
+    RGB r = smulf(v, (1 - ds) * (1 - dt));
+    r = sadd(r, smulf(v, (1 - ds) * dt));
+    r = sadd(r, smulf(v, ds * (1 - dt)));
+    r = sadd(r, smulf(v, ds * dt));
+    return r;
+}
+/* MIPMap::Lookup(st, width) (mipmap.h:245-261): every width < 1 is level < 0 here */
+static RGB lmap_lookup(const Inf* I, float st0, float st1) { return lmap_triangle(I->L, st0, st1); }
+
+static float spherical_theta(V3 v) { return acosf(clampf11(v.z)); }          /* geometry.h:1636-1638 */
+static float spherical_phi(V3 v) {                                           /* geometry.h:1640-1643 */
+    float p = atan2f(v.y, v.x);
+    return (p < 0) ? (p + 2 * PI_F) : p;
+}
+#define INV2PI_F 0.15915494309189533577f /* pbrt.h */
+
+/* Distribution1D::SampleContinuous (sampling.h:71-89) */
+static float dist1d_sample_cont(const float* func, const float* cdf, float funcInt, int n, float u, float* pdf,
+                                int* off) {
+    int offset = find_interval_cdf(cdf, n + 1, u);
+    if (off) *off = offset;
+    float du = u - cdf[offset];
+    if ((cdf[offset + 1] - cdf[offset]) > 0) du /= (cdf[offset + 1] - cdf[offset]);
+    if (pdf) *pdf = (funcInt > 0) ? func[offset] / funcInt : 0;
+    return (offset + du) / n;
+}
+
+/* InfiniteAreaLight ctor (sampling image + Distribution2D) and Preprocess */
+static void inf_init(Scene* sc, int li) {
+    const pt_light* l = &sc->d->lights[li];
+    Inf* I = &sc->inf[li];
+    I->L = rgbv(l->L);
+    I->l2w = xf_from(&l->light_to_world);
+    /* Scene::WorldBound() = BVH root bounds; Bounds3::BoundingSphere (geometry.h:959-962) */
+    if (sc->nnodes > 0) {
+        V3 pmin = sc->nodes[0].bounds.pmin, pmax = sc->nodes[0].bounds.pmax;
+        I->center = vmul(vadd(pmin, pmax), 0.5f);
+        int inside = I->center.x >= pmin.x && I->center.x <= pmax.x && I->center.y >= pmin.y &&
+                     I->center.y <= pmax.y && I->center.z >= pmin.z && I->center.z <= pmax.z;
+        I->radius = inside ? vlen(vsub(I->center, pmax)) : 0;
+    } else {
+        /* empty Bounds3f: pMin = +max, pMax = -max: center 0, not inside */
+        I->center = v3(0, 0, 0);
+        I->radius = 0;
+    }
+    /* img[u + v*width] = Lmap->Lookup((up, vp), fwidth).y() * sin(Pi (v+.5)/height) */
+    const int width = 2, height = 2;
+    float img[4];
+    for (int v = 0; v < height; ++v) {
+        float vp = (v + .5f) / (float)height;
+        float sinTheta = sinf(PI_F * (v + .5f) / height);
+        for (int u = 0; u < width; ++u) {
+            float up = (u + .5f) / (float)width;
+            img[u + v * width] = sy(lmap_lookup(I, up, vp));
+            img[u + v * width] *= sinTheta;
+        }
+    }
+    for (int v = 0; v < height; ++v) {
+        for (int u = 0; u < width; ++u) I->cfunc[v][u] = img[v * width + u];
+        dist1d_build(I->cfunc[v], width, I->ccdf[v], &I->cint[v]);
+        I->mfunc[v] = I->cint[v];
+    }
+    dist1d_build(I->mfunc, height, I->mcdf, &I->mint);
+}
+/* InfiniteAreaLight::Le (infinite.cpp:91-95) */
+static RGB inf_Le(const Inf* I, V3 d) {
+    V3 w = vnorm(xf_vec(&I->l2w.mi, d));
+    return lmap_lookup(I, spherical_phi(w) * INV2PI_F, spherical_theta(w) * INVPI_F);
+}
+/* InfiniteAreaLight::Sample_Li (infinite.cpp:97-121); *sp is the visibility
+ * target ref.p + wi * 2 worldRadius (zero error bounds and normal) */
+static RGB inf_sample_li(const Inf* I, const SI* ref, const float* u, V3* wi, float* pdf, V3* sp) {
+    float pdfs[2];
+    int v;
+    float d1 = dist1d_sample_cont(I->mfunc, I->mcdf, I->mint, 2, u[1], &pdfs[1], &v);
+    float d0 = dist1d_sample_cont(I->cfunc[v], I->ccdf[v], I->cint[v], 2, u[0], &pdfs[0], NULL);
+    float mapPdf = pdfs[0] * pdfs[1];
+    if (mapPdf == 0) { *pdf = 0; return rgb1(0.f); }
+    float theta = d1 * PI_F, phi = d0 * 2 * PI_F;
+    float cosTheta = cosf(theta), sinTheta = sinf(theta);
+    float sinPhi = sinf(phi), cosPhi = cosf(phi);
+    *wi = xf_vec(&I->l2w.m, v3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+    *pdf = mapPdf / (2 * PI_F * PI_F * sinTheta);
+    if (sinTheta == 0) *pdf = 0;
+    *sp = vadd(ref->p, vmul(*wi, 2 * I->radius));
+    return lmap_lookup(I, d0, d1);
+}
+/* InfiniteAreaLight::Pdf_Li (infinite.cpp:123-131) + Distribution2D::Pdf (sampling.h:136-142) */
+static float inf_pdf_li(const Inf* I, V3 w) {
+    V3 wi = xf_vec(&I->l2w.mi, w);
+    float theta = spherical_theta(wi), phi = spherical_phi(wi);
+    float sinTheta = sinf(theta);
+    if (sinTheta == 0) return 0;
+    float p0 = phi * INV2PI_F, p1 = theta * INVPI_F;
+    int iu = (int)(p0 * 2), iv = (int)(p1 * 2);
+    iu = iu < 0 ? 0 : (iu > 1 ? 1 : iu);
+    iv = iv < 0 ? 0 : (iv > 1 ? 1 : iv);
+    return (I->cfunc[iv][iu] / I->mint) / (2 * PI_F * PI_F * sinTheta);
+}
+
 /* DiffuseAreaLight::Sample_Li (diffuse.cpp:69-84) + Shape::Sample(ref,u,pdf) (shape.cpp:56-74) */
 static RGB area_sample_li(const Scene* sc, const pt_light* l, const SI* ref, const float* u, V3* wi, float* pdf,
                           V3* sp, V3* sn, V3* spErr) {
     V3 p, n, pe;
+    if (l->kind == PT_LIGHT_INFINITE) {
+        *sn = v3(0, 0, 0);
+        *spErr = v3(0, 0, 0);
+        return inf_sample_li(&sc->inf[l - sc->d->lights], ref, u, wi, pdf, sp);
+    }
     if (l->kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l->shape, u, &p, &n, &pe, pdf);
     else plane_sample(&sc->planes[l->shape], u, &p, &n, &pe, pdf);
     V3 w = vsub(p, ref->p);
@@ -1376,6 +1500,7 @@ static RGB area_sample_li(const Scene* sc, const pt_light* l, const SI* ref, con
 
 /* Shape::Pdf(ref, wi) (shape.cpp:76-91) for a triangle light */
 static float area_pdf_li(const Scene* sc, const pt_light* l, const SI* ref, V3 wi) {
+    if (l->kind == PT_LIGHT_INFINITE) return inf_pdf_li(&sc->inf[l - sc->d->lights], wi);
     Ray r = spawn_ray(ref->p, ref->pError, ref->n, wi);
     SI isl;
     float tHit;
@@ -1435,6 +1560,8 @@ static RGB estimate_direct_mis(const Scene* sc, const SI* it, const BSDF* bsdf, 
             RGB Li2 = rgb1(0);
             if (found) {
                 if (si_light(sc, &lis) == lightIdx) Li2 = si_Le(sc, &lis, vneg(wi));
+            } else if (l->kind == PT_LIGHT_INFINITE) {
+                Li2 = inf_Le(&sc->inf[lightIdx], r.d); /* light.Le(ray) */
             }
             if (!sblack(Li2)) {
                 Ld = sadd(Ld, sdivf(smulf(smul(smul(f, Li2), rgb1(1)), scatteringWeight), scatteringPdf));
@@ -1551,7 +1678,10 @@ static RGB path_li(const Scene* sc, Ray ray, Samp* smp, Counters* ctr) {
         int found = scene_intersect(sc, &ray, &isect, ctr);
         if (bounces == 0 || specularBounce) {
             if (found) L = sadd(L, smul(beta, si_Le(sc, &isect, vneg(ray.d))));
-            /* no infinite lights in the supported subset */
+            else
+                for (int li = 0; li < sc->d->n_lights; ++li) /* scene.infiniteLights, in light order */
+                    if (sc->d->lights[li].kind == PT_LIGHT_INFINITE)
+                        L = sadd(L, smul(beta, inf_Le(&sc->inf[li], ray.d)));
         }
         if (!found || bounces >= sc->max_depth) break;
         int mi = si_material(sc, &isect);
@@ -1798,13 +1928,22 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
         }
     }
     build_bvh(sc);
+    sc->inf = (struct Inf*)calloc((size_t)(d->n_lights + 1), sizeof(Inf));
+    for (int i = 0; i < d->n_lights; ++i)
+        if (d->lights[i].kind == PT_LIGHT_INFINITE) inf_init(sc, i);
     /* light distribution: "uniform" (lightdistrib.cpp:68-75) or "power" (integrator.cpp:515-522) */
     sc->nlights = d->n_lights;
     sc->ldist_func = (float*)calloc((size_t)(d->n_lights + 1), sizeof(float));
     sc->ldist_cdf = (float*)calloc((size_t)(d->n_lights + 2), sizeof(float));
     for (int i = 0; i < d->n_lights; ++i) {
-        if (d->integrator.light_strategy == PT_LIGHTS_POWER) {
+        if (d->integrator.light_strategy == PT_LIGHTS_POWER && d->n_lights > 1) { /* lightdistrib.cpp:47-50 */
             const pt_light* l = &d->lights[i];
+            if (l->kind == PT_LIGHT_INFINITE) {
+                /* InfiniteAreaLight::Power() = Pi r^2 Lmap->Lookup((.5,.5), .5) (infinite.cpp:85-89) */
+                const Inf* I = &sc->inf[i];
+                sc->ldist_func[i] = sy(smulf(lmap_lookup(I, .5f, .5f), PI_F * I->radius * I->radius));
+                continue;
+            }
             float area = l->kind == PT_LIGHT_DIFFUSE_AREA ? sc->tri_area[l->shape] : sc->planes[l->shape].area;
             /* DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:62-64) */
             RGB pw = smulf(smulf(smulf(rgbv(l->L), (float)(l->two_sided ? 2 : 1)), area), PI_F);
@@ -1835,7 +1974,7 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
 static void scene_free(Scene* sc) {
     free(sc->planes); free(sc->tri_area); free(sc->portal_planes);
     free(sc->prim_kind); free(sc->prim_index); free(sc->nodes);
-    free(sc->ldist_func); free(sc->ldist_cdf);
+    free(sc->ldist_func); free(sc->ldist_cdf); free(sc->inf);
 }
 
 typedef struct {

@@ -592,10 +592,80 @@ __device__ __forceinline__ void tri_sample(const DevScene& sc, int ti, float u0,
     *pdf = 1 / sc.tri_area[ti];
 }
 
+// ----------------------------------------------------------------------------
+// InfiniteAreaLight with a constant 1x1 Lmap (lights/infinite.cpp:43-132)
+// ----------------------------------------------------------------------------
+// MIPMap::triangle at level 0 of a 1x1 map, ImageWrap::Repeat (mipmap.h:264-274)
+PTHD S3 lmap_triangle(S3 v, float st0, float st1) {
+    const float s = st0 * 1 - 0.5f, t = st1 * 1 - 0.5f;
+    const int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    const float ds = s - s0, dt = t - t0;
+    S3 r = v * ((1 - ds) * (1 - dt));
+    r = r + v * ((1 - ds) * dt);
+    r = r + v * (ds * (1 - dt));
+    r = r + v * (ds * dt);
+    return r;
+}
+PTHD float spherical_theta(V3 v) { return libm_acosf(v.z < -1 ? -1.f : (v.z > 1 ? 1.f : v.z)); }  // geometry.h:1636
+PTHD float spherical_phi(V3 v) {                                                                  // geometry.h:1640
+    const float p = libm_atan2f(v.y, v.x);
+    return (p < 0) ? (p + 2 * kPi) : p;
+}
+constexpr float kInv2Pi = 0.15915494309189533577f;
+// Distribution1D::SampleContinuous (sampling.h:71-89) over n entries
+PTHD float dist1d_sample_cont(const float* func, const float* cdf, float funcInt, int n, float u, float* pdf, int* off) {
+    const int offset = find_interval(cdf, n + 1, u);
+    if (off) *off = offset;
+    float du = u - cdf[offset];
+    if ((cdf[offset + 1] - cdf[offset]) > 0) du /= (cdf[offset + 1] - cdf[offset]);
+    if (pdf) *pdf = (funcInt > 0) ? func[offset] / funcInt : 0;
+    return (offset + du) / n;
+}
+// InfiniteAreaLight::Le (infinite.cpp:91-95)
+__device__ __forceinline__ S3 inf_Le(const DevLight& l, V3 d) {
+    const V3 w = normalize(xf_vector(l.w2l, d));
+    return lmap_triangle(l.L, spherical_phi(w) * kInv2Pi, spherical_theta(w) * kInvPi);
+}
+// InfiniteAreaLight::Sample_Li (infinite.cpp:97-121); *sp is the visibility
+// target ref.p + wi * 2 worldRadius (zero error bounds and normal)
+__device__ __forceinline__ S3 inf_sample_li(const DevLight& l, V3 refp, float u0, float u1, V3* wi, float* pdf,
+                                            V3* sp) {
+    float pdf0, pdf1;
+    int v;
+    const float d1 = dist1d_sample_cont(l.mfunc, l.mcdf, l.mint, 2, u1, &pdf1, &v);
+    const float d0 = dist1d_sample_cont(l.cfunc + 2 * v, l.ccdf + 3 * v, l.cint[v], 2, u0, &pdf0, nullptr);
+    const float mapPdf = pdf0 * pdf1;
+    if (mapPdf == 0) { *pdf = 0; return s3(0.f); }
+    const float theta = d1 * kPi, phi = d0 * 2 * kPi;
+    const float cosTheta = libm_cosf(theta), sinTheta = libm_sinf(theta);
+    const float sinPhi = libm_sinf(phi), cosPhi = libm_cosf(phi);
+    *wi = xf_vector(l.l2w, v3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+    *pdf = mapPdf / (2 * kPi * kPi * sinTheta);
+    if (sinTheta == 0) *pdf = 0;
+    *sp = refp + *wi * (2 * l.radius);
+    return lmap_triangle(l.L, d0, d1);
+}
+// InfiniteAreaLight::Pdf_Li (infinite.cpp:123-131) + Distribution2D::Pdf (sampling.h:136-142)
+__device__ __forceinline__ float inf_pdf_li(const DevLight& l, V3 w) {
+    const V3 wi = xf_vector(l.w2l, w);
+    const float theta = spherical_theta(wi), phi = spherical_phi(wi);
+    const float sinTheta = libm_sinf(theta);
+    if (sinTheta == 0) return 0;
+    int iu = (int)(phi * kInv2Pi * 2), iv = (int)(theta * kInvPi * 2);
+    iu = iu < 0 ? 0 : (iu > 1 ? 1 : iu);
+    iv = iv < 0 ? 0 : (iv > 1 ? 1 : iv);
+    return (l.cfunc[2 * iv + iu] / l.mint) / (2 * kPi * kPi * sinTheta);
+}
+
 // DiffuseAreaLight::Sample_Li + Shape::Sample(ref, u, pdf) (diffuse.cpp:69-84, shape.cpp:56-74)
 __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, float u0,
                                              float u1, V3* wi, float* pdf, V3* sp, V3* sn, V3* spe) {
     V3 p, n, pe;
+    if (l.kind == PT_LIGHT_INFINITE) {
+        *sn = v3(0, 0, 0);
+        *spe = v3(0, 0, 0);
+        return inf_sample_li(l, ref.p, u0, u1, wi, pdf, sp);
+    }
     if (l.kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l.shape, u0, u1, &p, &n, &pe, pdf);
     else plane_sample(sc.planes[l.shape], u0, u1, &p, &n, &pe, pdf);
     V3 w = p - ref.p;
@@ -613,6 +683,7 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
 
 // Shape::Pdf(ref, wi) for the light's shape (shape.cpp:76-91)
 __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, V3 wi) {
+    if (l.kind == PT_LIGHT_INFINITE) return inf_pdf_li(l, wi);
     Ray r{offset_ray_origin(ref.p, ref.perr, ref.n, wi), wi, kInf};
     SurfHit isl;
     bool ok;

@@ -32,6 +32,12 @@ struct DevLight {
     int first_portal;
     int n_portals;
     float area;
+    // InfiniteAreaLight (lights/infinite.cpp) with a constant 1x1 Lmap
+    M4 l2w, w2l;
+    V3 center;
+    float radius;
+    float cfunc[4], ccdf[6], cint[2];  // Distribution2D conditionals (2 x 2)
+    float mfunc[2], mcdf[3], mint;     // and marginal
 };
 
 // Prim record flags (word 0 .w of the 48-byte record)

@@ -630,11 +630,14 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
             Ld = Ld + s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
         if (fl & kNfB) {
             const int h = ps.hitB[slot];
+            const int nl = __float_as_int(nee[kNeeLight * N + slot]);
             S3 Li = s3(0.f);
             if (h >= 0) {
                 int lid;
                 const S3 le = hit_Le(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
-                if (lid == __float_as_int(nee[kNeeLight * N + slot])) Li = le;
+                if (lid == nl) Li = le;
+            } else if (sc.lights[nl].kind == PT_LIGHT_INFINITE) {
+                Li = inf_Le(sc.lights[nl], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
             }
             if (!is_black(Li)) {
                 const S3 f2 = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
@@ -832,6 +835,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         if (found) prim_info(sc, hp, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
+            else
+                for (int li = 0; li < sc.n_lights; ++li)  // scene.infiniteLights, in light order
+                    if (sc.lights[li].kind == PT_LIGHT_INFINITE) L = L + beta * inf_Le(sc.lights[li], ray.d);
         }
         if (found && bounces < sc.max_depth) {
             if (sc.mats[mat].kind == PT_MAT_NONE) {

@@ -578,7 +578,7 @@ class Loader {
                 std::string n = read_string(tk);
                 Directive tmp;
                 params(&tmp, n);
-                throw PtError(PT_ERR_UNSUPPORTED, "LightSource \"" + n + "\" is outside the supported subset");
+                light_source(n, tmp.ps);
             } else if (d == "Shape") {
                 std::string n = read_string(tk);
                 Directive tmp;
@@ -785,6 +785,29 @@ class Loader {
         }
     }
 
+    // MakeLight (api.cpp) with the CTM as LightToWorld; lights keep
+    // declaration order (RenderOptions::lights).
+    void light_source(const std::string& name, const ParamSet& ps) {
+        if (!inWorld_) throw PtError(PT_ERR_PARSE, "LightSource outside WorldBegin");
+        if (name == "infinite" || name == "exinfinite") {
+            // CreateInfiniteLight (infinite.cpp:185-196)
+            if (!ps.string1("mapname", "").empty())
+                throw PtError(PT_ERR_UNSUPPORTED, "infinite light \"mapname\" (image maps) is outside the supported subset");
+            pt_light L{};
+            L.kind = PT_LIGHT_INFINITE;
+            float Lv[3] = {1, 1, 1}, sc[3] = {1, 1, 1};
+            ps.spectrum("L", Lv);
+            ps.spectrum("scale", sc);
+            for (int i = 0; i < 3; ++i) L.L[i] = Lv[i] * sc[i];
+            L.n_samples = std::max(1, ps.int1("samples", ps.int1("nsamples", 1)));
+            L.shape = -1;
+            store_xf(ctm_, &L.light_to_world);
+            out_->lights.push_back(L);
+            return;
+        }
+        throw PtError(PT_ERR_UNSUPPORTED, "LightSource \"" + name + "\" is outside the supported subset");
+    }
+
     static void diffuse_params(const ParamSet& ps, pt_light* L) {  // CreateDiffuseAreaLight (diffuse.cpp)
         float Lv[3] = {1, 1, 1}, sc[3] = {1, 1, 1};
         ps.spectrum("L", Lv);
@@ -792,6 +815,8 @@ class Loader {
         for (int i = 0; i < 3; ++i) L->L[i] = Lv[i] * sc[i];
         L->two_sided = ps.bool1("twosided", false) ? 1 : 0;
         L->strategy = PT_PORTAL_LIGHT;
+        L->n_samples = std::max(1, ps.int1("samples", ps.int1("nsamples", 1)));  // Light ctor (light.h)
+        store_xf(hxf_identity(), &L->light_to_world);
     }
 
     void portal_params(const ParamSet& ps, pt_light* L) {  // CreateAAPortal (portal_arealight.cpp:245-300)

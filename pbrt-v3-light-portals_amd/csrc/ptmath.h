@@ -303,6 +303,129 @@ PTHD int find_interval(const float* cdf, int size, float u) {
     return r > size - 2 ? size - 2 : r;
 }
 
+// ---- acosf / atanf / atan2f as the reference binary's libm computes them ------
+// glibc's flt-32 e_acosf.c, s_atanf.c and e_atan2f.c (the fdlibm float
+// algorithms): needed bit-exact for SphericalTheta / SphericalPhi
+// (geometry.h) in the infinite light.  Validated against the host libm by
+// tests/test_oracle_known_answers.py.
+constexpr float kAcPi = 3.1415925026e+00f, kAcPio2Hi = 1.5707962513e+00f, kAcPio2Lo = 7.5497894159e-08f;
+constexpr float kAcP0 = 1.6666667163e-01f, kAcP1 = -3.2556581497e-01f, kAcP2 = 2.0121252537e-01f,
+                kAcP3 = -4.0055535734e-02f, kAcP4 = 7.9153501429e-04f, kAcP5 = 3.4793309169e-05f;
+constexpr float kAcQ1 = -2.4033949375e+00f, kAcQ2 = 2.0209457874e+00f, kAcQ3 = -6.8828397989e-01f,
+                kAcQ4 = 7.7038154006e-02f;
+PTHD float libm_acosf(float x) {
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix == 0x3f800000) return hx > 0 ? 0.0f : kAcPi + 2.0f * kAcPio2Lo;
+    if (ix > 0x3f800000) return (x - x) / (x - x);
+    if (ix < 0x3f000000) {
+        if (ix <= 0x32800000) return kAcPio2Hi + kAcPio2Lo;
+        const float z = x * x;
+        const float p = z * (kAcP0 + z * (kAcP1 + z * (kAcP2 + z * (kAcP3 + z * (kAcP4 + z * kAcP5)))));
+        const float q = 1.0f + z * (kAcQ1 + z * (kAcQ2 + z * (kAcQ3 + z * kAcQ4)));
+        const float r = p / q;
+        return kAcPio2Hi - (x - (kAcPio2Lo - x * r));
+    } else if (hx < 0) {
+        const float z = (1.0f + x) * 0.5f;
+        const float p = z * (kAcP0 + z * (kAcP1 + z * (kAcP2 + z * (kAcP3 + z * (kAcP4 + z * kAcP5)))));
+        const float q = 1.0f + z * (kAcQ1 + z * (kAcQ2 + z * (kAcQ3 + z * kAcQ4)));
+        const float sq = sqrtf(z);
+        const float r = p / q;
+        const float w = r * sq - kAcPio2Lo;
+        return kAcPi - 2.0f * (sq + w);
+    } else {
+        const float z = (1.0f - x) * 0.5f;
+        const float sq = sqrtf(z);
+        const float df = u2f(f2u(sq) & 0xfffff000u);
+        const float c = (z - df * df) / (sq + df);
+        const float p = z * (kAcP0 + z * (kAcP1 + z * (kAcP2 + z * (kAcP3 + z * (kAcP4 + z * kAcP5)))));
+        const float q = 1.0f + z * (kAcQ1 + z * (kAcQ2 + z * (kAcQ3 + z * kAcQ4)));
+        const float r = p / q;
+        const float w = r * sq + c;
+        return 2.0f * (df + w);
+    }
+}
+PTHD float libm_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+                aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+                aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+                aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
+            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+        } else {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
+            else { id = 3; x = -1.0f / x; }
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -zz : zz;
+}
+PTHD float libm_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+                pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)f2u(x), hy = (int32_t)f2u(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return libm_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        switch (m) {
+            case 0: case 1: return y;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            switch (m) {
+                case 0: return pi_o_4 + tiny;
+                case 1: return -pi_o_4 - tiny;
+                case 2: return 3.0f * pi_o_4 + tiny;
+                default: return -3.0f * pi_o_4 - tiny;
+            }
+        }
+        switch (m) {
+            case 0: return 0.0f;
+            case 1: return -0.0f;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 23;
+    float z;
+    if (k > 26) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -26) z = 0.0f;
+    else z = libm_atanf(fabsf(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
 // ---- double-precision sin/cos for moderate arguments ---------------------------
 // The reference calls <math.h>'s double cos/sin in TrowbridgeReitzSample11
 // (phi in [0, 2pi)).  These follow the classic fdlibm kernels (k_sin.c,

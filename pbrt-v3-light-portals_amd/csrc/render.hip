@@ -208,6 +208,50 @@ namespace pt {
 
 static int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// InfiniteAreaLight ctor + Preprocess (infinite.cpp:43-83): LightToWorld,
+// world bounding sphere of the BVH root, and the Distribution2D over the 2x2
+// sin(theta)-weighted luminance image of the constant map.
+static void init_infinite(const pt_light& l, const std::vector<LinearNode>& nodes, DevLight* dl) {
+    std::memcpy(dl->l2w.m, l.light_to_world.m, 64);
+    std::memcpy(dl->w2l.m, l.light_to_world.minv, 64);
+    if (!nodes.empty()) {
+        const V3 pmin = v3(nodes[0].bmin[0], nodes[0].bmin[1], nodes[0].bmin[2]);
+        const V3 pmax = v3(nodes[0].bmax[0], nodes[0].bmax[1], nodes[0].bmax[2]);
+        dl->center = (pmin + pmax) * 0.5f;  // Bounds3::BoundingSphere (geometry.h:959-962)
+        const V3 c = dl->center;
+        const bool inside = c.x >= pmin.x && c.x <= pmax.x && c.y >= pmin.y && c.y <= pmax.y && c.z >= pmin.z &&
+                            c.z <= pmax.z;
+        dl->radius = inside ? len(c - pmax) : 0.f;
+    } else {
+        dl->center = v3(0, 0, 0);
+        dl->radius = 0.f;
+    }
+    const int width = 2, height = 2;
+    float img[4];
+    for (int v = 0; v < height; ++v) {
+        const float vp = (v + .5f) / (float)height;
+        const float sinTheta = std::sin(kPi * (v + .5f) / height);
+        for (int u = 0; u < width; ++u) {
+            const float up = (u + .5f) / (float)width;
+            img[u + v * width] = lum_y(lmap_triangle(dl->L, up, vp));
+            img[u + v * width] *= sinTheta;
+        }
+    }
+    auto build1d = [](const float* f, int n, float* cdf, float* funcInt) {  // Distribution1D (sampling.h:57-69)
+        cdf[0] = 0;
+        for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + f[i - 1] / n;
+        *funcInt = cdf[n];
+        if (*funcInt == 0) { for (int i = 1; i < n + 1; ++i) cdf[i] = (float)i / (float)n; }
+        else { for (int i = 1; i < n + 1; ++i) cdf[i] /= *funcInt; }
+    };
+    for (int v = 0; v < height; ++v) {
+        for (int u = 0; u < width; ++u) dl->cfunc[2 * v + u] = img[v * width + u];
+        build1d(dl->cfunc + 2 * v, width, dl->ccdf + 3 * v, &dl->cint[v]);
+        dl->mfunc[v] = dl->cint[v];
+    }
+    build1d(dl->mfunc, height, dl->mcdf, &dl->mint);
+}
+
 static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     if (!d) throw PtError(PT_ERR_INVALID_ARG, "null scene description");
     if (d->n_prims < 0 || d->n_triangles < 0 || d->n_planes < 0 || d->n_lights < 0 || d->n_materials < 0)
@@ -252,7 +296,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
             if (l.n_portals < 0 || l.n_portals > kMaxPortals || l.first_portal < 0 ||
                 l.first_portal + l.n_portals > d->n_portals)
                 throw PtError(PT_ERR_INVALID_ARG, "bad portal range");
-        } else
+        } else if (l.kind != PT_LIGHT_INFINITE)
             throw PtError(PT_ERR_UNSUPPORTED, "unsupported light kind");
     }
     if (d->sampler.spp <= 0) throw PtError(PT_ERR_INVALID_ARG, "spp must be > 0");
@@ -360,7 +404,8 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         dl.strategy = l.strategy;
         dl.first_portal = l.first_portal;
         dl.n_portals = l.n_portals;
-        if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
+        if (l.kind == PT_LIGHT_INFINITE) init_infinite(l, s->host_nodes, &dl);
+        else if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
         else {
             dl.area = planes[l.shape].area;
             const pt_aaplane& lp = d->planes[l.shape];
@@ -386,6 +431,10 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         if (d->integrator.light_strategy == PT_LIGHTS_POWER && nl > 1) {
             for (int i = 0; i < nl; ++i) {
                 const DevLight& l = lights[i];
+                if (l.kind == PT_LIGHT_INFINITE) {  // InfiniteAreaLight::Power (infinite.cpp:85-89)
+                    func[i] = lum_y(lmap_triangle(l.L, .5f, .5f) * (kPi * l.radius * l.radius));
+                    continue;
+                }
                 S3 pw = ((l.L * (float)(l.two_sided ? 2 : 1)) * l.area) * kPi;  // DiffuseAreaLight::Power
                 func[i] = lum_y(pw);
             }
