@@ -59,7 +59,11 @@ enum pt_prim_kind { PT_PRIM_TRIANGLE = 0, PT_PRIM_AAPLANE = 1 };
 enum pt_material_kind {
     PT_MAT_NONE = 0,   /* "" / "none": null BSDF, path passes through   */
     PT_MAT_MATTE = 1,  /* MatteMaterial  src/materials/matte.cpp:45-62 */
-    PT_MAT_METAL = 2   /* MetalMaterial  src/materials/metal.cpp:58-79 */
+    PT_MAT_METAL = 2,  /* MetalMaterial  src/materials/metal.cpp:58-79 */
+    PT_MAT_GLASS = 3,  /* GlassMaterial  src/materials/glass.cpp:45-83 */
+    PT_MAT_DISPERSIVE_GLASS = 4, /* DispersiveGlassMaterial  src/materials/dispersive_glass.cpp:48-123 */
+    PT_MAT_MIRROR = 5, /* MirrorMaterial  src/materials/mirror.cpp:44-52 */
+    PT_MAT_PLASTIC = 6 /* PlasticMaterial  src/materials/plastic.cpp:45-70 */
 };
 
 enum pt_light_kind {
@@ -123,8 +127,16 @@ typedef struct pt_material {
     float sigma;     /* matte: OrenNayar sigma in degrees; only 0 supported */
     float eta[3];    /* metal: constant eta */
     float k[3];      /* metal: constant k */
-    float alpha[2];  /* metal: TrowbridgeReitz alphax, alphay (after RoughnessToAlpha
-                        when remaproughness, and the 0.001 floor of the ctor) */
+    float alpha[2];  /* metal / plastic / rough glass: TrowbridgeReitz alphax, alphay
+                        (after RoughnessToAlpha when remaproughness, and the 0.001
+                        floor of the ctor) */
+    float ks[3];     /* plastic: constant Ks */
+    float kr[3];     /* glass / dispersive / mirror: constant Kr */
+    float kt[3];     /* glass / dispersive: constant Kt */
+    float ior;       /* glass: "eta" / "index" */
+    float ior_min;   /* dispersive: "etaMin" / "indexMin" */
+    float ior_max;   /* dispersive: "etaMax" / "indexMax" */
+    int32_t specular;/* glass / dispersive: uroughness == 0 && vroughness == 0 */
 } pt_material;
 
 /* AAPortal (src/portals/aaportal.h) as parsed from portalData. */

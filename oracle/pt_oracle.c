@@ -1221,37 +1221,261 @@ static RGB frConductor(float cosThetaI, RGB etai, RGB etat, RGB k) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* BSDF (core/reflection.{h,cpp}; materials/matte.cpp, materials/metal.cpp)   */
+/* BSDF (core/reflection.{h,cpp}) and the materials that build it:           */
+/* matte.cpp, metal.cpp, glass.cpp, dispersive_glass.cpp, mirror.cpp,         */
+/* plastic.cpp.  A BSDF holds up to two BxDFs ("lobes").                      */
 /* ------------------------------------------------------------------------ */
+/* BxDFType (reflection.h:70-77) */
+#define BX_REFLECTION 1
+#define BX_TRANSMISSION 2
+#define BX_DIFFUSE 4
+#define BX_GLOSSY 8
+#define BX_SPECULAR 16
+#define BX_ALL 31
+enum { LB_LAMBERT = 1, LB_MFREFL, LB_MFTRANS, LB_FRESNELSPEC, LB_SPECREFL };
+enum { FR_NOOP = 0, FR_CONDUCTOR, FR_DIELECTRIC };
 typedef struct {
-    int nbxdf;       /* 0 or 1 BxDF */
-    int metal;       /* 0: LambertianReflection(R); 1: MicrofacetReflection(R=1, TR, FresnelConductor) */
-    RGB R;
-    RGB eta, k;
-    float ax, ay;
+    int kind, type, fres;
+    RGB R;               /* R (reflection) or T (transmission) scale */
+    RGB T;               /* FresnelSpecular's T */
+    RGB feta, fk;        /* FresnelConductor(1, eta, k) */
+    float fetaI, fetaT;  /* FresnelDielectric(etaI, etaT) */
+    float etaA, etaB;    /* transmission lobes */
+    float ax, ay;        /* TrowbridgeReitz */
+} Lobe;
+typedef struct {
+    int n;
+    Lobe lb[2];
+    float eta;           /* BSDF::eta */
     V3 ns, ng, ss, ts;
 } BSDF;
 
-/* MatteMaterial / MetalMaterial ::ComputeScatteringFunctions (matte.cpp:45-62,
- * metal.cpp:58-79) + BSDF ctor (reflection.h:167-172) */
-static void make_bsdf(const pt_material* m, const SI* si, BSDF* b) {
+/* FrDielectric (reflection.cpp:47-69) */
+static float frDielectric(float cosThetaI, float etaI, float etaT) {
+    cosThetaI = clampf11(cosThetaI);
+    int entering = cosThetaI > 0.f;
+    if (!entering) { float t = etaI; etaI = etaT; etaT = t; cosThetaI = fabsf(cosThetaI); }
+    float sinThetaI = sqrtf(fmaxs((float)0, 1 - cosThetaI * cosThetaI));
+    float sinThetaT = etaI / etaT * sinThetaI;
+    if (sinThetaT >= 1) return 1;
+    float cosThetaT = sqrtf(fmaxs((float)0, 1 - sinThetaT * sinThetaT));
+    float Rparl = ((etaT * cosThetaI) - (etaI * cosThetaT)) / ((etaT * cosThetaI) + (etaI * cosThetaT));
+    float Rperp = ((etaI * cosThetaI) - (etaT * cosThetaT)) / ((etaI * cosThetaI) + (etaT * cosThetaT));
+    return (Rparl * Rparl + Rperp * Rperp) / 2;
+}
+static RGB fresnel_eval(const Lobe* l, float cosThetaI) {
+    if (l->fres == FR_CONDUCTOR) return frConductor(fabsf(cosThetaI), rgb1(1.), l->feta, l->fk); /* reflection.cpp:118-120 */
+    if (l->fres == FR_DIELECTRIC) return rgb1(frDielectric(cosThetaI, l->fetaI, l->fetaT));      /* :128-130 */
+    return rgb1(1.);                                                                            /* FresnelNoOp */
+}
+/* Refract (reflection.h:97-108) */
+static int refract(V3 wi, V3 n, float eta, V3* wt) {
+    float cosThetaI = vdot(n, wi);
+    float sin2ThetaI = fmaxs((float)0, (float)(1 - cosThetaI * cosThetaI));
+    float sin2ThetaT = eta * eta * sin2ThetaI;
+    if (sin2ThetaT >= 1) return 0;
+    float cosThetaT = sqrtf(1 - sin2ThetaT);
+    *wt = vadd(vmul(vneg(wi), eta), vmul(n, eta * cosThetaI - cosThetaT));
+    return 1;
+}
+static int same_hemi(V3 w, V3 wp) { return w.z * wp.z > 0; }
+
+/* MicrofacetReflection::f (reflection.cpp:259-271) */
+static RGB mfrefl_f(const Lobe* l, V3 wo, V3 wi) {
+    float cosThetaO = fabsf(wo.z), cosThetaI = fabsf(wi.z);
+    V3 wh = vadd(wi, wo);
+    if (cosThetaI == 0 || cosThetaO == 0) return rgb1(0.);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return rgb1(0.);
+    wh = vnorm(wh);
+    V3 whf = vdot(wh, v3(0, 0, 1)) < 0.f ? vneg(wh) : wh; /* Faceforward */
+    RGB F = fresnel_eval(l, vdot(wi, whf));
+    return sdivf(smul(smulf(smulf(l->R, trD(l->ax, l->ay, wh)), trG(l->ax, l->ay, wo, wi)), F),
+                 4 * cosThetaI * cosThetaO);
+}
+/* MicrofacetTransmission::f (reflection.cpp:279-303) */
+static RGB mftrans_f(const Lobe* l, V3 wo, V3 wi) {
+    if (same_hemi(wo, wi)) return rgb1(0);
+    float cosThetaO = wo.z, cosThetaI = wi.z;
+    if (cosThetaI == 0 || cosThetaO == 0) return rgb1(0);
+    float eta = wo.z > 0 ? (l->etaB / l->etaA) : (l->etaA / l->etaB);
+    V3 wh = vnorm(vadd(wo, vmul(wi, eta)));
+    if (wh.z < 0) wh = vneg(wh);
+    if (vdot(wo, wh) * vdot(wi, wh) > 0) return rgb1(0);
+    RGB F = rgb1(frDielectric(vdot(wo, wh), l->etaA, l->etaB));
+    float sqrtDenom = vdot(wo, wh) + eta * vdot(wi, wh);
+    float factor = 1 / eta; /* TransportMode::Radiance */
+    float v = fabsf(trD(l->ax, l->ay, wh) * trG(l->ax, l->ay, wo, wi) * eta * eta * vabsdot(wi, wh) *
+                    vabsdot(wo, wh) * factor * factor / (cosThetaI * cosThetaO * sqrtDenom * sqrtDenom));
+    return smulf(smul(ssub(rgb1(1.f), F), l->R), v);
+}
+static float mftrans_pdf(const Lobe* l, V3 wo, V3 wi) { /* reflection.cpp:479-493 */
+    if (same_hemi(wo, wi)) return 0;
+    float eta = wo.z > 0 ? (l->etaB / l->etaA) : (l->etaA / l->etaB);
+    V3 wh = vnorm(vadd(wo, vmul(wi, eta)));
+    if (vdot(wo, wh) * vdot(wi, wh) > 0) return 0;
+    float sqrtDenom = vdot(wo, wh) + eta * vdot(wi, wh);
+    float dwh_dwi = fabsf((eta * eta * vdot(wi, wh)) / (sqrtDenom * sqrtDenom));
+    return trPdf(l->ax, l->ay, wo, wh) * dwh_dwi;
+}
+/* BxDF::f */
+static RGB lobe_f(const Lobe* l, V3 wo, V3 wi) {
+    switch (l->kind) {
+        case LB_LAMBERT: return smulf(l->R, INVPI_F);
+        case LB_MFREFL: return mfrefl_f(l, wo, wi);
+        case LB_MFTRANS: return mftrans_f(l, wo, wi);
+        default: return rgb1(0.f); /* specular lobes: delta distributions */
+    }
+}
+/* BxDF::Pdf */
+static float lobe_pdf(const Lobe* l, V3 wo, V3 wi) {
+    switch (l->kind) {
+        case LB_LAMBERT: return same_hemi(wo, wi) ? fabsf(wi.z) * INVPI_F : 0; /* reflection.cpp:425-427 */
+        case LB_MFREFL: { /* reflection.cpp:458-462 */
+            if (!same_hemi(wo, wi)) return 0;
+            V3 wh = vnorm(vadd(wo, wi));
+            return trPdf(l->ax, l->ay, wo, wh) / (4 * vdot(wo, wh));
+        }
+        case LB_MFTRANS: return mftrans_pdf(l, wo, wi);
+        default: return 0;
+    }
+}
+/* BxDF::Sample_f; *type may be narrowed (FresnelSpecular) */
+static RGB lobe_sample(const Lobe* l, V3 wo, V3* wi, const float* u, float* pdf, int* type) {
+    switch (l->kind) {
+        case LB_LAMBERT: { /* reflection.cpp:416-423 */
+            *wi = cosine_sample_hemisphere(u);
+            if (wo.z < 0) wi->z *= -1;
+            *pdf = lobe_pdf(l, wo, *wi);
+            return lobe_f(l, wo, *wi);
+        }
+        case LB_MFREFL: { /* reflection.cpp:443-456 */
+            if (wo.z == 0) return rgb1(0.);
+            V3 wh = trSampleWh(l->ax, l->ay, wo, u);
+            if (vdot(wo, wh) < 0) return rgb1(0.);
+            *wi = vadd(vneg(wo), vmul(wh, 2 * vdot(wo, wh))); /* Reflect */
+            if (!same_hemi(wo, *wi)) return rgb1(0.f);
+            *pdf = trPdf(l->ax, l->ay, wo, wh) / (4 * vdot(wo, wh));
+            return mfrefl_f(l, wo, *wi);
+        }
+        case LB_MFTRANS: { /* reflection.cpp:466-477 */
+            if (wo.z == 0) return rgb1(0.);
+            V3 wh = trSampleWh(l->ax, l->ay, wo, u);
+            if (vdot(wo, wh) < 0) return rgb1(0.);
+            float eta = wo.z > 0 ? (l->etaA / l->etaB) : (l->etaB / l->etaA);
+            if (!refract(wo, wh, eta, wi)) return rgb1(0.);
+            *pdf = mftrans_pdf(l, wo, *wi);
+            return mftrans_f(l, wo, *wi);
+        }
+        case LB_SPECREFL: { /* SpecularReflection::Sample_f (reflection.h:400-410) */
+            *wi = v3(-wo.x, -wo.y, wo.z);
+            *pdf = 1;
+            return sdivf(smul(fresnel_eval(l, wi->z), l->R), fabsf(wi->z));
+        }
+        case LB_FRESNELSPEC: { /* FresnelSpecular::Sample_f (reflection.cpp:520-554) */
+            float F = frDielectric(wo.z, l->etaA, l->etaB);
+            if (u[0] < F) {
+                *wi = v3(-wo.x, -wo.y, wo.z);
+                *type = BX_SPECULAR | BX_REFLECTION;
+                *pdf = F;
+                return sdivf(smulf(l->R, F), fabsf(wi->z));
+            } else {
+                int entering = wo.z > 0;
+                float etaI = entering ? l->etaA : l->etaB;
+                float etaT = entering ? l->etaB : l->etaA;
+                V3 n = vdot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1); /* Faceforward(n, wo) */
+                if (!refract(wo, n, etaI / etaT, wi)) return rgb1(0);
+                RGB ft = smulf(l->T, 1 - F); /* T * (1 - F) */
+                ft = smulf(ft, (etaI * etaI) / (etaT * etaT)); /* TransportMode::Radiance */
+                *type = BX_SPECULAR | BX_TRANSMISSION;
+                *pdf = 1 - F;
+                return sdivf(ft, fabsf(wi->z));
+            }
+        }
+    }
+    return rgb1(0.f);
+}
+
+static void add_lobe(BSDF* b, int kind, int type, RGB R) {
+    Lobe* l = &b->lb[b->n++];
+    memset(l, 0, sizeof *l);
+    l->kind = kind; l->type = type; l->R = R;
+}
+static RGB clamp0(RGB r) { /* Spectrum::Clamp() */
+    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : (r.c[i] > INFINITY ? INFINITY : r.c[i]);
+    return r;
+}
+/* Material::ComputeScatteringFunctions(si, arena, Radiance, allowMultipleLobes = true)
+ * + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength. */
+static void make_bsdf(const pt_material* m, const SI* si, float wvl0, BSDF* b) {
     b->ns = si->sn; b->ng = si->n;
     b->ss = vnorm(si->sdpdu);
     b->ts = vcross(b->ns, b->ss);
-    b->nbxdf = 0;
-    b->metal = m->kind == PT_MAT_METAL;
-    if (b->metal) {
-        b->nbxdf = 1;
-        b->R = rgb1(1.);
-        b->eta = rgbv(m->eta);
-        b->k = rgbv(m->k);
-        b->ax = m->alpha[0];
-        b->ay = m->alpha[1];
-        return;
+    b->n = 0;
+    b->eta = 1;
+    switch (m->kind) {
+        case PT_MAT_MATTE: { /* matte.cpp:45-62, sigma = 0 */
+            RGB r = clamp0(rgbv(m->kd));
+            if (!sblack(r)) add_lobe(b, LB_LAMBERT, BX_REFLECTION | BX_DIFFUSE, r);
+            break;
+        }
+        case PT_MAT_METAL: { /* metal.cpp:58-79 */
+            add_lobe(b, LB_MFREFL, BX_REFLECTION | BX_GLOSSY, rgb1(1.));
+            Lobe* l = &b->lb[0];
+            l->fres = FR_CONDUCTOR; l->feta = rgbv(m->eta); l->fk = rgbv(m->k);
+            l->ax = m->alpha[0]; l->ay = m->alpha[1];
+            break;
+        }
+        case PT_MAT_MIRROR: { /* mirror.cpp:44-52 */
+            RGB r = clamp0(rgbv(m->kr));
+            if (!sblack(r)) { add_lobe(b, LB_SPECREFL, BX_REFLECTION | BX_SPECULAR, r); b->lb[0].fres = FR_NOOP; }
+            break;
+        }
+        case PT_MAT_PLASTIC: { /* plastic.cpp:45-70 */
+            RGB kd = clamp0(rgbv(m->kd));
+            if (!sblack(kd)) add_lobe(b, LB_LAMBERT, BX_REFLECTION | BX_DIFFUSE, kd);
+            RGB ks = clamp0(rgbv(m->ks));
+            if (!sblack(ks)) {
+                add_lobe(b, LB_MFREFL, BX_REFLECTION | BX_GLOSSY, ks);
+                Lobe* l = &b->lb[b->n - 1];
+                l->fres = FR_DIELECTRIC; l->fetaI = 1.5f; l->fetaT = 1.f;
+                l->ax = m->alpha[0]; l->ay = m->alpha[1];
+            }
+            break;
+        }
+        case PT_MAT_GLASS:
+        case PT_MAT_DISPERSIVE_GLASS: { /* glass.cpp:45-83, dispersive_glass.cpp:48-123 (bsdf[0]) */
+            float eta = m->ior;
+            if (m->kind == PT_MAT_DISPERSIVE_GLASS) {
+                const float lminsq = (float)(400 * 400), lmaxsq = (float)(700 * 700);
+                const float cauchyB = (lminsq * m->ior_max - lmaxsq * m->ior_min) / (lminsq - lmaxsq);
+                const float cauchyC = lminsq * (m->ior_max - cauchyB);
+                eta = cauchyB + cauchyC / (wvl0 * wvl0);
+            }
+            b->eta = eta;
+            RGB R = clamp0(rgbv(m->kr)), T = clamp0(rgbv(m->kt));
+            if (sblack(R) && sblack(T)) break;
+            if (m->specular) {
+                add_lobe(b, LB_FRESNELSPEC, BX_REFLECTION | BX_TRANSMISSION | BX_SPECULAR, R);
+                b->lb[0].etaA = 1.f; b->lb[0].etaB = eta;
+                b->lb[0].T = T;
+            } else {
+                if (!sblack(R)) {
+                    add_lobe(b, LB_MFREFL, BX_REFLECTION | BX_GLOSSY, R);
+                    Lobe* l = &b->lb[b->n - 1];
+                    l->fres = FR_DIELECTRIC; l->fetaI = 1.f; l->fetaT = eta;
+                    l->ax = m->alpha[0]; l->ay = m->alpha[1];
+                }
+                if (!sblack(T)) {
+                    add_lobe(b, LB_MFTRANS, BX_TRANSMISSION | BX_GLOSSY, T);
+                    Lobe* l = &b->lb[b->n - 1];
+                    l->etaA = 1.f; l->etaB = eta;
+                    l->ax = m->alpha[0]; l->ay = m->alpha[1];
+                }
+            }
+            break;
+        }
+        default: break;
     }
-    RGB r = rgbv(m->kd);
-    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : (r.c[i] > INFINITY ? INFINITY : r.c[i]); /* Clamp() */
-    if (!sblack(r)) { b->nbxdf = 1; b->R = r; }
 }
 static V3 w2l(const BSDF* b, V3 v) { return v3(vdot(v, b->ss), vdot(v, b->ts), vdot(v, b->ns)); }
 static V3 l2w(const BSDF* b, V3 v) {
@@ -1259,78 +1483,65 @@ static V3 l2w(const BSDF* b, V3 v) {
               b->ss.y * v.x + b->ts.y * v.y + b->ns.y * v.z,
               b->ss.z * v.x + b->ts.z * v.y + b->ns.z * v.z);
 }
-/* MicrofacetReflection::f (reflection.cpp:259-271) */
-static RGB mf_f(const BSDF* b, V3 wo, V3 wi) {
-    float cosThetaO = fabsf(wo.z), cosThetaI = fabsf(wi.z);
-    V3 wh = vadd(wi, wo);
-    if (cosThetaI == 0 || cosThetaO == 0) return rgb1(0.);
-    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return rgb1(0.);
-    wh = vnorm(wh);
-    V3 whf = vdot(wh, v3(0, 0, 1)) < 0.f ? vneg(wh) : wh; /* Faceforward */
-    RGB F = frConductor(fabsf(vdot(wi, whf)), rgb1(1.), b->eta, b->k); /* FresnelConductor::Evaluate */
-    return sdivf(smul(smulf(smulf(b->R, trD(b->ax, b->ay, wh)), trG(b->ax, b->ay, wo, wi)), F),
-                 4 * cosThetaI * cosThetaO);
+static int lobe_matches(const Lobe* l, int flags) { return (l->type & flags) == l->type; }
+static int bsdf_num(const BSDF* b, int flags) { /* BSDF::NumComponents */
+    int n = 0;
+    for (int i = 0; i < b->n; ++i) n += lobe_matches(&b->lb[i], flags);
+    return n;
 }
-static RGB bxdf_f(const BSDF* b, V3 wo, V3 wi) {
-    return b->metal ? mf_f(b, wo, wi) : smulf(b->R, INVPI_F);
-}
-static float bxdf_pdf(const BSDF* b, V3 wo, V3 wi) {
-    if (b->metal) { /* MicrofacetReflection::Pdf (reflection.cpp:458-462) */
-        if (!(wo.z * wi.z > 0)) return 0;
-        V3 wh = vnorm(vadd(wo, wi));
-        return trPdf(b->ax, b->ay, wo, wh) / (4 * vdot(wo, wh));
-    }
-    return (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0; /* BxDF::Pdf (reflection.cpp:425-427) */
-}
-/* Both BxDFs are non-specular reflection lobes: they match BSDF_ALL and
- * BSDF_ALL & ~BSDF_SPECULAR. */
-static RGB bsdf_f(const BSDF* b, V3 woW, V3 wiW) { /* reflection.cpp:713-726 */
+static RGB bsdf_f(const BSDF* b, V3 woW, V3 wiW, int flags) { /* reflection.cpp:713-726 */
     V3 wi = w2l(b, wiW), wo = w2l(b, woW);
     if (wo.z == 0) return rgb1(0);
     int reflect = vdot(wiW, b->ng) * vdot(woW, b->ng) > 0;
     RGB f = rgb1(0);
-    if (b->nbxdf && reflect) f = sadd(f, bxdf_f(b, wo, wi));
+    for (int i = 0; i < b->n; ++i) {
+        const Lobe* l = &b->lb[i];
+        if (lobe_matches(l, flags) && ((reflect && (l->type & BX_REFLECTION)) || (!reflect && (l->type & BX_TRANSMISSION))))
+            f = sadd(f, lobe_f(l, wo, wi));
+    }
     return f;
 }
-static float bsdf_pdf(const BSDF* b, V3 woW, V3 wiW) { /* reflection.cpp:814-829 */
-    if (b->nbxdf == 0) return 0.f;
+static float bsdf_pdf(const BSDF* b, V3 woW, V3 wiW, int flags) { /* reflection.cpp:814-829 */
+    if (b->n == 0) return 0.f;
     V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return 0.;
     float pdf = 0.f;
     int matching = 0;
-    ++matching;
-    pdf += bxdf_pdf(b, wo, wi);
+    for (int i = 0; i < b->n; ++i)
+        if (lobe_matches(&b->lb[i], flags)) { ++matching; pdf += lobe_pdf(&b->lb[i], wo, wi); }
     return matching > 0 ? pdf / matching : 0.f;
 }
-/* BSDF::Sample_f (reflection.cpp:747-812) with BxDF::Sample_f (416-423) or
- * MicrofacetReflection::Sample_f (443-456). */
-static RGB bsdf_sample_f(const BSDF* b, V3 woW, V3* wiW, const float* u, float* pdf, int* sampled) {
-    if (b->nbxdf == 0) { *pdf = 0; *sampled = 0; return rgb1(0); }
-    int matchingComps = 1;
+/* BSDF::Sample_f (reflection.cpp:747-812); *sampled = the sampled BxDFType */
+static RGB bsdf_sample_f(const BSDF* b, V3 woW, V3* wiW, const float* u, float* pdf, int flags, int* sampled) {
+    int matchingComps = bsdf_num(b, flags);
+    if (matchingComps == 0) { *pdf = 0; *sampled = 0; return rgb1(0); }
     int comp = (int)floorf(u[0] * matchingComps);
     if (comp > matchingComps - 1) comp = matchingComps - 1;
+    const Lobe* bx = NULL;
+    int count = comp;
+    for (int i = 0; i < b->n; ++i)
+        if (lobe_matches(&b->lb[i], flags) && count-- == 0) { bx = &b->lb[i]; break; }
     float ur[2] = {fmins(u[0] * matchingComps - comp, ONE_MINUS_EPS), u[1]};
-    V3 wo = w2l(b, woW), wi;
+    V3 wo = w2l(b, woW), wi = v3(0, 0, 0);
     if (wo.z == 0) { *sampled = 0; return rgb1(0); }
     *pdf = 0;
-    *sampled = 1;
-    if (b->metal) {
-        if (wo.z == 0) return rgb1(0.);
-        V3 wh = trSampleWh(b->ax, b->ay, wo, ur);
-        if (vdot(wo, wh) < 0) return rgb1(0.);
-        wi = vadd(vneg(wo), vmul(wh, 2 * vdot(wo, wh))); /* Reflect (reflection.h:93-95) */
-        if (!(wo.z * wi.z > 0)) return rgb1(0.f);
-        *pdf = trPdf(b->ax, b->ay, wo, wh) / (4 * vdot(wo, wh));
-    } else {
-        wi = cosine_sample_hemisphere(ur);
-        if (wo.z < 0) wi.z *= -1;
-        *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * INVPI_F : 0;
-    }
+    *sampled = bx->type;
+    RGB f = lobe_sample(bx, wo, &wi, ur, pdf, sampled);
     if (*pdf == 0) { *sampled = 0; return rgb1(0); }
     *wiW = l2w(b, wi);
-    int reflect = vdot(*wiW, b->ng) * vdot(woW, b->ng) > 0;
-    RGB f = rgb1(0);
-    if (reflect) f = sadd(f, bxdf_f(b, wo, wi));
+    if (!(bx->type & BX_SPECULAR) && matchingComps > 1)
+        for (int i = 0; i < b->n; ++i)
+            if (&b->lb[i] != bx && lobe_matches(&b->lb[i], flags)) *pdf += lobe_pdf(&b->lb[i], wo, wi);
+    if (matchingComps > 1) *pdf /= matchingComps;
+    if (!(bx->type & BX_SPECULAR)) {
+        int reflect = vdot(*wiW, b->ng) * vdot(woW, b->ng) > 0;
+        f = rgb1(0.);
+        for (int i = 0; i < b->n; ++i) {
+            const Lobe* l = &b->lb[i];
+            if (lobe_matches(l, flags) && ((reflect && (l->type & BX_REFLECTION)) || (!reflect && (l->type & BX_TRANSMISSION))))
+                f = sadd(f, lobe_f(l, wo, wi));
+        }
+    }
     return f;
 }
 
@@ -1531,8 +1742,8 @@ static RGB estimate_direct_mis(const Scene* sc, const SI* it, const BSDF* bsdf, 
     V3 sp, sn, spe;
     RGB Li = area_sample_li(sc, l, it, uLight, &wi, &lightPdf, &sp, &sn, &spe);
     if (lightPdf > 0 && !sblack(Li)) {
-        RGB f = smulf(bsdf_f(bsdf, it->wo, wi), vabsdot(wi, it->sn));
-        scatteringPdf = bsdf_pdf(bsdf, it->wo, wi);
+        RGB f = smulf(bsdf_f(bsdf, it->wo, wi, BX_ALL & ~BX_SPECULAR), vabsdot(wi, it->sn));
+        scatteringPdf = bsdf_pdf(bsdf, it->wo, wi, BX_ALL & ~BX_SPECULAR);
         if (!sblack(f)) {
             /* VisibilityTester::Unoccluded -> SpawnRayTo(Interaction) (light.cpp:59-61, interaction.h:75-80) */
             V3 origin = offset_ray_origin(it->p, it->pError, it->n, vsub(sp, it->p));
@@ -1547,7 +1758,7 @@ static RGB estimate_direct_mis(const Scene* sc, const SI* it, const BSDF* bsdf, 
     }
     {
         int sampledType = 0;
-        RGB f = bsdf_sample_f(bsdf, it->wo, &wi, uScattering, &scatteringPdf, &sampledType);
+        RGB f = bsdf_sample_f(bsdf, it->wo, &wi, uScattering, &scatteringPdf, BX_ALL & ~BX_SPECULAR, &sampledType);
         f = smulf(f, vabsdot(wi, it->sn));
         if (!sblack(f) && scatteringPdf > 0) {
             scatteringWeight = 1;
@@ -1639,7 +1850,7 @@ static RGB estimate_direct_portal(const Scene* sc, const SI* it, const BSDF* bsd
                     SI lis;
                     Ray r = spawn_ray(it->p, it->pError, it->n, wi);
                     if (scene_intersect(sc, &r, &lis, ctr)) Li = si_Le(sc, &lis, vneg(wi));
-                    RGB f = smulf(bsdf_f(bsdf, it->wo, wi), vabsdot(wi, it->sn));
+                    RGB f = smulf(bsdf_f(bsdf, it->wo, wi, BX_ALL & ~BX_SPECULAR), vabsdot(wi, it->sn));
                     if (!sblack(f) && !sblack(Li)) Ld = sadd(Ld, sdivf(smul(f, Li), pdf));
                 }
                 if (l->strategy == PT_PORTAL_PROJECTION) Ld = sdivf(Ld, portalPdf);
@@ -1657,7 +1868,7 @@ static RGB estimate_direct_portal(const Scene* sc, const SI* it, const BSDF* bsd
             SI lis;
             Ray r = spawn_ray(it->p, it->pError, it->n, wi);
             if (scene_intersect(sc, &r, &lis, ctr)) Li = si_Le(sc, &lis, vneg(wi));
-            RGB f = smulf(bsdf_f(bsdf, it->wo, wi), vabsdot(wi, it->sn));
+            RGB f = smulf(bsdf_f(bsdf, it->wo, wi, BX_ALL & ~BX_SPECULAR), vabsdot(wi, it->sn));
             if (!sblack(f) && !sblack(Li)) Ld = sadd(Ld, sdivf(smul(f, Li), pdf));
         }
     }
@@ -1667,7 +1878,7 @@ static RGB estimate_direct_portal(const Scene* sc, const SI* it, const BSDF* bsd
 /* ------------------------------------------------------------------------ */
 /* PathIntegrator::Li (path.cpp:64-189)                                      */
 /* ------------------------------------------------------------------------ */
-static RGB path_li(const Scene* sc, Ray ray, Samp* smp, Counters* ctr) {
+static RGB path_li(const Scene* sc, Ray ray, float wvl0, Samp* smp, Counters* ctr) {
     RGB L = rgb1(0), beta = rgb1(1);
     int specularBounce = 0;
     int bounces;
@@ -1692,8 +1903,8 @@ static RGB path_li(const Scene* sc, Ray ray, Samp* smp, Counters* ctr) {
             continue;
         }
         BSDF bsdf;
-        make_bsdf(mat, &isect, &bsdf);
-        if (bsdf.nbxdf > 0) { /* NumComponents(BSDF_ALL & ~BSDF_SPECULAR) > 0 */
+        make_bsdf(mat, &isect, wvl0, &bsdf);
+        if (bsdf_num(&bsdf, BX_ALL & ~BX_SPECULAR) > 0) {
             /* UniformSampleOneLight (integrator.cpp:100-122) */
             RGB Ld = rgb1(0);
             if (nLights > 0) {
@@ -1719,10 +1930,14 @@ static RGB path_li(const Scene* sc, Ray ray, Samp* smp, Counters* ctr) {
         int sampled = 0;
         float u[2];
         get2d(smp, u);
-        RGB f = bsdf_sample_f(&bsdf, wo, &wi, u, &pdf, &sampled);
+        RGB f = bsdf_sample_f(&bsdf, wo, &wi, u, &pdf, BX_ALL, &sampled);
         if (sblack(f) || pdf == 0.f) break;
         beta = smul(beta, sdivf(smulf(f, vabsdot(wi, isect.sn)), pdf));
-        specularBounce = 0; /* Lambertian only */
+        specularBounce = (sampled & BX_SPECULAR) != 0;
+        if ((sampled & BX_SPECULAR) && (sampled & BX_TRANSMISSION)) {
+            float eta = bsdf.eta;
+            etaScale *= (vdot(wo, isect.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+        }
         ray = spawn_ray(isect.p, isect.pError, isect.n, wi);
         RGB rrBeta = smulf(beta, etaScale);
         if (smaxc(rrBeta) < sc->rr_threshold && bounces > 3) {
@@ -1874,10 +2089,12 @@ static void render_tile(const Scene* sc, const Halton* h, int tx, int ty, FilmTi
                 float fx = (float)x + uf[0], fy = (float)y + uf[1];
                 (void)get1d(&smp);               /* time */
                 get2d(&smp, ul);                 /* pLens */
-                (void)get1d(&smp);               /* wvl (fork, sampler.cpp:51) */
+                float uw = get1d(&smp);          /* wvl (fork, sampler.cpp:51) */
+                /* Camera::GenerateWvls (camera.cpp:62-76): only wvls[0] is used on the RGB path */
+                float wvl0 = (float)400 + (float)300 * uw;
                 Ray r = camera_ray(sc, fx, fy, ul);
                 ctr->camera++;
-                RGB L = path_li(sc, r, &smp, ctr);
+                RGB L = path_li(sc, r, wvl0, &smp, ctr);
                 /* radiance sanitiser (integrator.cpp:592-613) */
                 if (snan(L)) L = rgb1(0);
                 else if (sy(L) < -1e-5) L = rgb1(0);
@@ -2110,7 +2327,7 @@ static void local_bsdf(const pt_material* m, BSDF* b) {
     SI si;
     memset(&si, 0, sizeof si);
     si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
-    make_bsdf(m, &si, b);
+    make_bsdf(m, &si, 550.f, b);
 }
 /* Batched BSDF hook with the layout of the product's pt_debug_bsdf: per record
  * in8 = wo[3], wi[3], u0, u1 -> out8 = f[3], pdf, sampled wi[3], sampled pdf
@@ -2126,12 +2343,12 @@ int oracle_bsdf_batch(const pt_scene_desc* d, int mat, int n, const float* in8, 
         RGB f = rgb1(0);
         float pdf = 0;
         int zero = wi.x == 0 && wi.y == 0 && wi.z == 0;
-        if (!zero) { f = bsdf_f(&b, wo, wi); pdf = bsdf_pdf(&b, wo, wi); }
+        if (!zero) { f = bsdf_f(&b, wo, wi, BX_ALL); pdf = bsdf_pdf(&b, wo, wi, BX_ALL); }
         float u[2] = {a[6], a[7]};
         V3 ws = v3(0, 0, 0);
         float spdf = 0;
         int sampled = 0;
-        RGB sf = bsdf_sample_f(&b, wo, &ws, u, &spdf, &sampled);
+        RGB sf = bsdf_sample_f(&b, wo, &ws, u, &spdf, BX_ALL, &sampled);
         if (zero) f = sf;
         o[0] = f.c[0]; o[1] = f.c[1]; o[2] = f.c[2]; o[3] = pdf;
         o[4] = ws.x; o[5] = ws.y; o[6] = ws.z; o[7] = spdf;

@@ -433,114 +433,309 @@ __device__ __forceinline__ S3 fr_conductor(float cosThetaI, S3 etat, S3 k) {
 }
 
 // ----------------------------------------------------------------------------
-// BSDF (reflection.{h,cpp}): one BxDF per material --
-//   matte: LambertianReflection(Kd)                     (matte.cpp:45-62)
-//   metal: MicrofacetReflection(1, TrowbridgeReitz, FresnelConductor(1, eta, k))
-//                                                       (metal.cpp:58-79)
+// BSDF (reflection.{h,cpp}) with up to two BxDFs ("lobes"), built by the
+// materials matte.cpp, metal.cpp, glass.cpp, dispersive_glass.cpp (bsdf[0]),
+// mirror.cpp, plastic.cpp.  Lobe parameters are read from the material record
+// when evaluated.
 // ----------------------------------------------------------------------------
+constexpr int kBxR = 1, kBxT = 2, kBxDiffuse = 4, kBxGlossy = 8, kBxSpecular = 16, kBxAll = 31;  // BxDFType
+constexpr int kBxNonSpecular = kBxAll & ~kBxSpecular;
+enum LobeKind { kLbLambert = 1, kLbMfRefl = 2, kLbMfTrans = 3, kLbFresnelSpec = 4, kLbSpecRefl = 5 };
+
+__device__ __forceinline__ int lobe_type(int k) {
+    switch (k) {
+        case kLbLambert: return kBxR | kBxDiffuse;
+        case kLbMfRefl: return kBxR | kBxGlossy;
+        case kLbMfTrans: return kBxT | kBxGlossy;
+        case kLbFresnelSpec: return kBxR | kBxT | kBxSpecular;
+        default: return kBxR | kBxSpecular;
+    }
+}
+__device__ __forceinline__ S3 clamp0(S3 r) {  // Spectrum::Clamp()
+    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : r.c[i];
+    return r;
+}
+
 struct Bsdf {
-    int nbxdf;
-    int kind;            // PT_MAT_MATTE / PT_MAT_METAL
-    S3 R;
+    int n;
+    int lk0, lk1;          // lobe kinds in BSDF::Add order (distinct within a BSDF)
+    float eta;             // BSDF::eta
     const pt_material* m;
     V3 ns, ng, ss, ts;
 };
 
-__device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, Bsdf* b) {
-    b->ns = si.sn;
-    b->ng = si.n;
-    b->ss = normalize(si.sdpdu);
-    b->ts = cross(b->ns, b->ss);
-    b->m = m;
-    b->kind = m->kind;
-    if (m->kind == PT_MAT_METAL) {
-        b->R = s3(1.f);
-        b->nbxdf = 1;
-    } else {
-        S3 r = s3(m->kd[0], m->kd[1], m->kd[2]);
-        for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : r.c[i];  // Spectrum::Clamp()
-        b->nbxdf = is_black(r) ? 0 : 1;
-        b->R = r;
+__device__ __forceinline__ V3 refl_z(V3 wo) { return v3(-wo.x, -wo.y, wo.z); }
+// FrDielectric (reflection.cpp:47-69)
+__device__ __forceinline__ float fr_dielectric(float cosThetaI, float etaI, float etaT) {
+    cosThetaI = clamp11(cosThetaI);
+    if (!(cosThetaI > 0.f)) {
+        const float t = etaI; etaI = etaT; etaT = t;
+        cosThetaI = fabsf(cosThetaI);
     }
+    const float sinThetaI = sqrtf(smax(0.f, 1 - cosThetaI * cosThetaI));
+    const float sinThetaT = etaI / etaT * sinThetaI;
+    if (sinThetaT >= 1) return 1;
+    const float cosThetaT = sqrtf(smax(0.f, 1 - sinThetaT * sinThetaT));
+    const float Rparl = ((etaT * cosThetaI) - (etaI * cosThetaT)) / ((etaT * cosThetaI) + (etaI * cosThetaT));
+    const float Rperp = ((etaI * cosThetaI) - (etaT * cosThetaT)) / ((etaI * cosThetaI) + (etaT * cosThetaT));
+    return (Rparl * Rparl + Rperp * Rperp) / 2;
 }
-__device__ __forceinline__ V3 w2l(const Bsdf& b, V3 v) { return v3(dot(v, b.ss), dot(v, b.ts), dot(v, b.ns)); }
-__device__ __forceinline__ V3 l2w(const Bsdf& b, V3 v) {
-    return v3(b.ss.x * v.x + b.ts.x * v.y + b.ns.x * v.z, b.ss.y * v.x + b.ts.y * v.y + b.ns.y * v.z,
-              b.ss.z * v.x + b.ts.z * v.y + b.ns.z * v.z);
+// Refract (reflection.h:97-108)
+__device__ __forceinline__ bool refract(V3 wi, V3 n, float eta, V3* wt) {
+    const float cosThetaI = dot(n, wi);
+    const float sin2ThetaI = smax(0.f, 1 - cosThetaI * cosThetaI);
+    const float sin2ThetaT = eta * eta * sin2ThetaI;
+    if (sin2ThetaT >= 1) return false;
+    const float cosThetaT = sqrtf(1 - sin2ThetaT);
+    *wt = (-wi) * eta + n * (eta * cosThetaI - cosThetaT);
+    return true;
 }
-// MicrofacetReflection::f (reflection.cpp:259-271), local frame
-__device__ __forceinline__ S3 mf_f(const Bsdf& b, V3 wo, V3 wi) {
+// Scale (R or T) and Fresnel term of the MicrofacetReflection lobe
+__device__ __forceinline__ S3 mfrefl_R(const Bsdf& b) {
+    const pt_material* m = b.m;
+    if (m->kind == PT_MAT_METAL) return s3(1.f);
+    if (m->kind == PT_MAT_PLASTIC) return clamp0(s3(m->ks[0], m->ks[1], m->ks[2]));
+    return clamp0(s3(m->kr[0], m->kr[1], m->kr[2]));
+}
+__device__ __forceinline__ S3 mfrefl_F(const Bsdf& b, float cosThetaI) {
+    const pt_material* m = b.m;
+    if (m->kind == PT_MAT_METAL)  // FresnelConductor::Evaluate (reflection.cpp:118-120)
+        return fr_conductor(fabsf(cosThetaI), s3(m->eta[0], m->eta[1], m->eta[2]), s3(m->k[0], m->k[1], m->k[2]));
+    if (m->kind == PT_MAT_PLASTIC) return s3(fr_dielectric(cosThetaI, 1.5f, 1.f));
+    return s3(fr_dielectric(cosThetaI, 1.f, b.eta));
+}
+// MicrofacetReflection::f (reflection.cpp:259-271)
+__device__ __forceinline__ S3 mfrefl_f(const Bsdf& b, V3 wo, V3 wi) {
     const float cosO = fabsf(wo.z), cosI = fabsf(wi.z);
     V3 wh = wi + wo;
     if (cosI == 0 || cosO == 0) return s3(0.f);
     if (wh.x == 0 && wh.y == 0 && wh.z == 0) return s3(0.f);
     wh = normalize(wh);
     const V3 whf = dot(wh, v3(0, 0, 1)) < 0.f ? -wh : wh;  // Faceforward(wh, (0,0,1))
+    const S3 F = mfrefl_F(b, dot(wi, whf));
+    const float ax = b.m->alpha[0], ay = b.m->alpha[1];
+    return mfrefl_R(b) * tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * F / (4 * cosI * cosO);
+}
+// MicrofacetTransmission::f / Pdf (reflection.cpp:279-303, 479-493); etaA = 1, etaB = eta
+__device__ __forceinline__ S3 mftrans_f(const Bsdf& b, V3 wo, V3 wi) {
+    if (wo.z * wi.z > 0) return s3(0.f);
+    const float cosO = wo.z, cosI = wi.z;
+    if (cosI == 0 || cosO == 0) return s3(0.f);
+    const float eta = wo.z > 0 ? (b.eta / 1.f) : (1.f / b.eta);
+    V3 wh = normalize(wo + wi * eta);
+    if (wh.z < 0) wh = -wh;
+    if (dot(wo, wh) * dot(wi, wh) > 0) return s3(0.f);
+    const S3 F = s3(fr_dielectric(dot(wo, wh), 1.f, b.eta));
+    const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+    const float factor = 1 / eta;  // TransportMode::Radiance
+    const float ax = b.m->alpha[0], ay = b.m->alpha[1];
+    const float v = fabsf(tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) *
+                          factor * factor / (cosI * cosO * sqrtDenom * sqrtDenom));
     const pt_material* m = b.m;
-    const S3 F = fr_conductor(fabsf(dot(wi, whf)), s3(m->eta[0], m->eta[1], m->eta[2]),
-                              s3(m->k[0], m->k[1], m->k[2]));
-    const float ax = m->alpha[0], ay = m->alpha[1];
-    return b.R * tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * F / (4 * cosI * cosO);
+    return ((s3(1.f) - F) * clamp0(s3(m->kt[0], m->kt[1], m->kt[2]))) * v;
 }
-// BxDF::f of the material's one BxDF (local frame)
-__device__ __forceinline__ S3 bxdf_f(const Bsdf& b, V3 wo, V3 wi) {
-    if (b.kind == PT_MAT_METAL) return mf_f(b, wo, wi);
-    return b.R * kInvPi;
+__device__ __forceinline__ float mftrans_pdf(const Bsdf& b, V3 wo, V3 wi) {
+    if (wo.z * wi.z > 0) return 0;
+    const float eta = wo.z > 0 ? (b.eta / 1.f) : (1.f / b.eta);
+    const V3 wh = normalize(wo + wi * eta);
+    if (dot(wo, wh) * dot(wi, wh) > 0) return 0;
+    const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+    const float dwh_dwi = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
+    return tr_pdf(b.m->alpha[0], b.m->alpha[1], wo, wh) * dwh_dwi;
 }
-__device__ __forceinline__ float bxdf_pdf(const Bsdf& b, V3 wo, V3 wi) {
-    if (b.kind == PT_MAT_METAL) {  // MicrofacetReflection::Pdf (reflection.cpp:458-462)
+__device__ __forceinline__ S3 lambert_R(const Bsdf& b) { return clamp0(s3(b.m->kd[0], b.m->kd[1], b.m->kd[2])); }
+
+__device__ __forceinline__ S3 lobe_f(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::f
+    if (k == kLbLambert) return lambert_R(b) * kInvPi;
+    if (k == kLbMfRefl) return mfrefl_f(b, wo, wi);
+    if (k == kLbMfTrans) return mftrans_f(b, wo, wi);
+    return s3(0.f);
+}
+__device__ __forceinline__ float lobe_pdf(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::Pdf
+    if (k == kLbLambert) return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    if (k == kLbMfRefl) {
         if (!(wo.z * wi.z > 0)) return 0.f;
         const V3 wh = normalize(wo + wi);
         return tr_pdf(b.m->alpha[0], b.m->alpha[1], wo, wh) / (4 * dot(wo, wh));
     }
-    return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;  // BxDF::Pdf (reflection.cpp:425-427)
+    if (k == kLbMfTrans) return mftrans_pdf(b, wo, wi);
+    return 0.f;
 }
-__device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW) {  // BSDF::f (reflection.cpp:713-726)
-    V3 wo = w2l(b, woW), wi = w2l(b, wiW);
+// BxDF::Sample_f; *type narrowed by FresnelSpecular
+__device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, float u0, float u1, float* pdf,
+                                          int* type) {
+    const pt_material* m = b.m;
+    if (k == kLbLambert) {
+        *wi = cosine_sample_hemisphere(u0, u1);
+        if (wo.z < 0) wi->z *= -1;
+        *pdf = lobe_pdf(b, k, wo, *wi);
+        return lobe_f(b, k, wo, *wi);
+    }
+    if (k == kLbMfRefl || k == kLbMfTrans) {
+        const float ax = m->alpha[0], ay = m->alpha[1];
+        if (wo.z == 0) return s3(0.f);
+        const V3 wh = tr_sample_wh(ax, ay, wo, u0, u1);
+        if (dot(wo, wh) < 0) return s3(0.f);
+        if (k == kLbMfRefl) {
+            *wi = -wo + (2 * dot(wo, wh)) * wh;  // Reflect
+            if (!(wo.z * wi->z > 0)) return s3(0.f);
+            *pdf = tr_pdf(ax, ay, wo, wh) / (4 * dot(wo, wh));
+            return mfrefl_f(b, wo, *wi);
+        }
+        const float eta = wo.z > 0 ? (1.f / b.eta) : (b.eta / 1.f);
+        if (!refract(wo, wh, eta, wi)) return s3(0.f);
+        *pdf = mftrans_pdf(b, wo, *wi);
+        return mftrans_f(b, wo, *wi);
+    }
+    if (k == kLbSpecRefl) {  // SpecularReflection::Sample_f, FresnelNoOp
+        *wi = refl_z(wo);
+        *pdf = 1;
+        return (s3(1.f) * clamp0(s3(m->kr[0], m->kr[1], m->kr[2]))) / fabsf(wi->z);
+    }
+    // FresnelSpecular::Sample_f (reflection.cpp:520-554), etaA = 1, etaB = eta
+    const float F = fr_dielectric(wo.z, 1.f, b.eta);
+    if (u0 < F) {
+        *wi = refl_z(wo);
+        *type = kBxSpecular | kBxR;
+        *pdf = F;
+        return (clamp0(s3(m->kr[0], m->kr[1], m->kr[2])) * F) / fabsf(wi->z);
+    }
+    const bool entering = wo.z > 0;
+    const float etaI = entering ? 1.f : b.eta;
+    const float etaT = entering ? b.eta : 1.f;
+    const V3 n = dot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1);  // Faceforward(n, wo)
+    if (!refract(wo, n, etaI / etaT, wi)) return s3(0.f);
+    S3 ft = clamp0(s3(m->kt[0], m->kt[1], m->kt[2])) * (1 - F);
+    ft = ft * ((etaI * etaI) / (etaT * etaT));  // TransportMode::Radiance
+    *type = kBxSpecular | kBxT;
+    *pdf = 1 - F;
+    return ft / fabsf(wi->z);
+}
+
+__device__ __forceinline__ void add_lobe(Bsdf* b, int k) {
+    if (b->n == 0) b->lk0 = k;
+    else b->lk1 = k;
+    ++b->n;
+}
+// Material::ComputeScatteringFunctions(..., Radiance, allowMultipleLobes = true)
+// + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength.
+__device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, float wvl0, Bsdf* b) {
+    b->ns = si.sn;
+    b->ng = si.n;
+    b->ss = normalize(si.sdpdu);
+    b->ts = cross(b->ns, b->ss);
+    b->m = m;
+    b->n = 0;
+    b->lk0 = b->lk1 = 0;
+    b->eta = 1;
+    const int kind = m->kind;
+    if (kind == PT_MAT_MATTE) {
+        if (!is_black(lambert_R(*b))) add_lobe(b, kLbLambert);
+    } else if (kind == PT_MAT_METAL) {
+        add_lobe(b, kLbMfRefl);
+    } else if (kind == PT_MAT_MIRROR) {
+        if (!is_black(clamp0(s3(m->kr[0], m->kr[1], m->kr[2])))) add_lobe(b, kLbSpecRefl);
+    } else if (kind == PT_MAT_PLASTIC) {
+        if (!is_black(lambert_R(*b))) add_lobe(b, kLbLambert);
+        if (!is_black(clamp0(s3(m->ks[0], m->ks[1], m->ks[2])))) add_lobe(b, kLbMfRefl);
+    } else if (kind == PT_MAT_GLASS || kind == PT_MAT_DISPERSIVE_GLASS) {
+        float eta = m->ior;
+        if (kind == PT_MAT_DISPERSIVE_GLASS) {  // Cauchy's equation (dispersive_glass.cpp:62-73)
+            const float lminsq = (float)(400 * 400), lmaxsq = (float)(700 * 700);
+            const float cauchyB = (lminsq * m->ior_max - lmaxsq * m->ior_min) / (lminsq - lmaxsq);
+            const float cauchyC = lminsq * (m->ior_max - cauchyB);
+            eta = cauchyB + cauchyC / (wvl0 * wvl0);
+        }
+        b->eta = eta;
+        const bool hasR = !is_black(clamp0(s3(m->kr[0], m->kr[1], m->kr[2])));
+        const bool hasT = !is_black(clamp0(s3(m->kt[0], m->kt[1], m->kt[2])));
+        if (!hasR && !hasT) return;
+        if (m->specular) {
+            add_lobe(b, kLbFresnelSpec);
+        } else {
+            if (hasR) add_lobe(b, kLbMfRefl);
+            if (hasT) add_lobe(b, kLbMfTrans);
+        }
+    }
+}
+__device__ __forceinline__ V3 w2l(const Bsdf& b, V3 v) { return v3(dot(v, b.ss), dot(v, b.ts), dot(v, b.ns)); }
+__device__ __forceinline__ int lobe_at(const Bsdf& b, int i) { return i == 0 ? b.lk0 : b.lk1; }
+__device__ __forceinline__ V3 l2w(const Bsdf& b, V3 v) {
+    return v3(b.ss.x * v.x + b.ts.x * v.y + b.ns.x * v.z, b.ss.y * v.x + b.ts.y * v.y + b.ns.y * v.z,
+              b.ss.z * v.x + b.ts.z * v.y + b.ns.z * v.z);
+}
+__device__ __forceinline__ bool lobe_matches(int k, int flags) { return (lobe_type(k) & flags) == lobe_type(k); }
+__device__ __forceinline__ int bsdf_num(const Bsdf& b, int flags) {  // BSDF::NumComponents
+    int n = 0;
+    for (int i = 0; i < 2; ++i)
+        if (i < b.n) n += lobe_matches(lobe_at(b, i), flags) ? 1 : 0;
+    return n;
+}
+__device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW, int flags) {  // reflection.cpp:713-726
+    const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return s3(0.f);
-    bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
     S3 f = s3(0.f);
-    if (b.nbxdf && reflect) f = f + bxdf_f(b, wo, wi);
+    for (int i = 0; i < 2; ++i) {
+        if (i >= b.n) break;
+        const int k = lobe_at(b, i), t = lobe_type(k);
+        if (lobe_matches(k, flags) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT)))) f = f + lobe_f(b, k, wo, wi);
+    }
     return f;
 }
-__device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW) {  // BSDF::Pdf (reflection.cpp:814-829)
-    if (b.nbxdf == 0) return 0.f;
-    V3 wo = w2l(b, woW), wi = w2l(b, wiW);
+__device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW, int flags) {  // reflection.cpp:814-829
+    if (b.n == 0) return 0.f;
+    const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return 0.f;
     float pdf = 0.f;
-    pdf += bxdf_pdf(b, wo, wi);
-    return pdf / 1;
-}
-// BSDF::Sample_f (reflection.cpp:747-812); *pdf is left at 0 wherever the
-// reference returns black before writing it.
-__device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf) {
-    if (b.nbxdf == 0) { *pdf = 0; return s3(0.f); }
-    int comp = (int)floorf(u0 * 1);
-    comp = (0 < comp) ? 0 : comp;  // std::min(comp, matchingComps - 1)
-    float ur0 = smin(u0 * 1 - comp, kOneMinusEps);
-    V3 wo = w2l(b, woW);
-    if (wo.z == 0) return s3(0.f);
-    *pdf = 0;
-    V3 wi;
-    if (b.kind == PT_MAT_METAL) {
-        // MicrofacetReflection::Sample_f (reflection.cpp:443-456)
-        const float ax = b.m->alpha[0], ay = b.m->alpha[1];
-        if (wo.z == 0) return s3(0.f);
-        const V3 wh = tr_sample_wh(ax, ay, wo, ur0, u1);
-        if (dot(wo, wh) < 0) return s3(0.f);
-        wi = -wo + (2 * dot(wo, wh)) * wh;  // Reflect
-        if (!(wo.z * wi.z > 0)) return s3(0.f);
-        *pdf = tr_pdf(ax, ay, wo, wh) / (4 * dot(wo, wh));
-    } else {
-        wi = cosine_sample_hemisphere(ur0, u1);
-        if (wo.z < 0) wi.z *= -1;
-        *pdf = (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    int matching = 0;
+    for (int i = 0; i < 2; ++i) {
+        if (i >= b.n) break;
+        const int k = lobe_at(b, i);
+        if (lobe_matches(k, flags)) { ++matching; pdf += lobe_pdf(b, k, wo, wi); }
     }
-    if (*pdf == 0) return s3(0.f);
+    return matching > 0 ? pdf / matching : 0.f;
+}
+// BSDF::Sample_f (reflection.cpp:747-812); *pdf stays 0 wherever the reference
+// returns black before writing it; *sampled is the sampled BxDFType.
+__device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf, int flags,
+                                          int* sampled) {
+    const int matchingComps = bsdf_num(b, flags);
+    if (matchingComps == 0) { *pdf = 0; *sampled = 0; return s3(0.f); }
+    int comp = (int)floorf(u0 * matchingComps);
+    comp = comp < matchingComps - 1 ? comp : matchingComps - 1;
+    int bk = b.lk0, count = comp;
+    for (int i = 0; i < 2; ++i) {
+        if (i >= b.n) break;
+        if (lobe_matches(lobe_at(b, i), flags) && count-- == 0) { bk = lobe_at(b, i); break; }
+    }
+    const float ur0 = smin(u0 * matchingComps - comp, kOneMinusEps);
+    const V3 wo = w2l(b, woW);
+    if (wo.z == 0) { *sampled = 0; return s3(0.f); }
+    *pdf = 0;
+    *sampled = lobe_type(bk);
+    V3 wi = v3(0, 0, 0);
+    S3 f = lobe_sample(b, bk, wo, &wi, ur0, u1, pdf, sampled);
+    if (*pdf == 0) { *sampled = 0; return s3(0.f); }
     *wiW = l2w(b, wi);
-    bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
-    S3 f = s3(0.f);
-    if (reflect) f = f + bxdf_f(b, wo, wi);
+    const bool spec = (lobe_type(bk) & kBxSpecular) != 0;
+    if (!spec && matchingComps > 1)
+        for (int i = 0; i < 2; ++i) {
+            if (i >= b.n) break;
+            const int k = lobe_at(b, i);
+            if (k != bk && lobe_matches(k, flags)) *pdf += lobe_pdf(b, k, wo, wi);
+        }
+    if (matchingComps > 1) *pdf /= matchingComps;
+    if (!spec) {
+        const bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
+        f = s3(0.f);
+        for (int i = 0; i < 2; ++i) {
+            if (i >= b.n) break;
+            const int k = lobe_at(b, i), t = lobe_type(k);
+            if (lobe_matches(k, flags) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT))))
+                f = f + lobe_f(b, k, wo, wi);
+        }
+    }
     return f;
 }
 

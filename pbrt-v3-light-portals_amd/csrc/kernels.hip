@@ -733,7 +733,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                 if (pdf > 0) {
                     const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
                     store_ray6(ps.rayA, N, slot, r);
-                    put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn));
+                    put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
                     put_nee(ps, slot, kNeePdf, pdf);
                     put_nee3(ps, slot, kNeeLi, s3(0.f));
                     flags |= kNfA;
@@ -750,7 +750,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
     if (!is_black(Li) && pdf > 0) {
         const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
         store_ray6(ps.rayA, N, slot, r);
-        put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn));
+        put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
         put_nee(ps, slot, kNeePdf, pdf);
         put_nee3(ps, slot, kNeeLi, Li);
         flags |= kNfA;
@@ -771,8 +771,8 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
     float lightPdf = 0, scatteringPdf = 0;
     const S3 Li = area_sample_li(sc, l, it, ul0, ul1, &wi, &lightPdf, &sp, &sn, &spe);
     if (lightPdf > 0 && !is_black(Li)) {
-        const S3 f = bsdf_f(bsdf, it.wo, wi) * absdot(wi, it.sn);
-        scatteringPdf = bsdf_pdf(bsdf, it.wo, wi);
+        const S3 f = bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn);
+        scatteringPdf = bsdf_pdf(bsdf, it.wo, wi, kBxNonSpecular);
         if (!is_black(f)) {
             // VisibilityTester::Unoccluded -> SpawnRayTo(Interaction) (light.cpp:59-61, interaction.h:75-80)
             const V3 origin = offset_ray_origin(it.p, it.perr, it.n, sp - it.p);
@@ -790,7 +790,8 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
     {
         float pdf2 = scatteringPdf;
         V3 wi2 = wi;
-        S3 f = bsdf_sample(bsdf, it.wo, &wi2, us0, us1, &pdf2);
+        int sampledType = 0;
+        S3 f = bsdf_sample(bsdf, it.wo, &wi2, us0, us1, &pdf2, kBxNonSpecular, &sampledType);
         f = f * absdot(wi2, it.sn);
         if (!is_black(f) && pdf2 > 0) {
             const float lp = area_pdf_li(sc, l, it, wi2);
@@ -849,8 +850,11 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
             } else {
                 Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
                 Bsdf bsdf;
-                make_bsdf(&sc.mats[mat], si, &bsdf);
-                if (bsdf.nbxdf > 0) {
+                // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
+                const float wvl0 = sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
+                                       ? (float)400 + (float)300 * halton_dim(sc, dm.idx, 5) : 550.f;
+                make_bsdf(&sc.mats[mat], si, wvl0, &bsdf);
+                if (bsdf_num(bsdf, kBxNonSpecular) > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
                     bool deferred = false;
                     float lightPdf = 0;
@@ -889,10 +893,16 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 const float u0 = dm.get1(), u1 = dm.get1();
                 V3 wi = v3(0, 0, 0);
                 float pdf = 0;
-                const S3 f = bsdf_sample(bsdf, -ray.d, &wi, u0, u1, &pdf);
+                int sampled = 0;
+                const S3 f = bsdf_sample(bsdf, -ray.d, &wi, u0, u1, &pdf, kBxAll, &sampled);
                 if (!(is_black(f) || pdf == 0.f)) {
                     beta = beta * ((f * absdot(wi, si.sn)) / pdf);
-                    st &= ~kStSpecular;
+                    if (sampled & kBxSpecular) st |= kStSpecular;
+                    else st &= ~kStSpecular;
+                    if ((sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
+                        const float eta = bsdf.eta;
+                        ps.eta[slot] *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                    }
                     const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     bool alive = true;
                     // Russian roulette (path.cpp:177-185)
@@ -1106,18 +1116,19 @@ __global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float
     SurfHit si{};
     si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
     Bsdf b;
-    make_bsdf(&sc.mats[mat], si, &b);
+    make_bsdf(&sc.mats[mat], si, 550.f, &b);
     const V3 wo = v3(a[0], a[1], a[2]), wi = v3(a[3], a[4], a[5]);
     float* o = out + 8 * i;
     S3 f = s3(0.f);
     float pdf = 0;
     if (wi.x != 0 || wi.y != 0 || wi.z != 0) {
-        f = bsdf_f(b, wo, wi);
-        pdf = bsdf_pdf(b, wo, wi);
+        f = bsdf_f(b, wo, wi, kBxAll);
+        pdf = bsdf_pdf(b, wo, wi, kBxAll);
     }
     V3 ws = v3(0, 0, 0);
     float spdf = 0;
-    const S3 sf = bsdf_sample(b, wo, &ws, a[6], a[7], &spdf);
+    int sampled = 0;
+    const S3 sf = bsdf_sample(b, wo, &ws, a[6], a[7], &spdf, kBxAll, &sampled);
     if (wi.x == 0 && wi.y == 0 && wi.z == 0) f = sf;
     o[0] = f.c[0]; o[1] = f.c[1]; o[2] = f.c[2]; o[3] = pdf;
     o[4] = ws.x; o[5] = ws.y; o[6] = ws.z; o[7] = spdf;

@@ -598,6 +598,23 @@ class Loader {
         }
     }
 
+    // TextureParams lookup order: shape parameters, then material parameters
+    float f1(const char* n, float def, bool* found, const ParamSet& shapeParams) const {
+        const Param* p = shapeParams.floats(n);
+        if (!p) p = gs_.materialParams.floats(n);
+        if (found) *found = p && !p->nums.empty();
+        return (p && !p->nums.empty()) ? (float)p->nums[0] : def;
+    }
+    void spectrum2(const char* n, float out[3], const ParamSet& shapeParams) const {
+        gs_.materialParams.spectrum(n, out);
+        shapeParams.spectrum(n, out);
+    }
+    void no_textures(std::initializer_list<const char*> names, const ParamSet& shapeParams) const {
+        for (const char* tex : names)
+            if (gs_.materialParams.find(tex, {"texture"}) || shapeParams.find(tex, {"texture"}))
+                throw PtError(PT_ERR_UNSUPPORTED, std::string("textured \"") + tex + "\" is outside the supported subset");
+    }
+
     int material_for(const ParamSet& shapeParams) {
         // GraphicsState::GetMaterialForShape: shape params may override the
         // current material's parameters (api.cpp, TextureParams lookup order).
@@ -632,15 +649,9 @@ class Loader {
             hasK = shapeParams.spectrum("k", k) || hasK;
             if (!hasEta || !hasK)
                 throw PtError(PT_ERR_UNSUPPORTED, "metal needs rgb \"eta\" and \"k\" (the copper default is spectral)");
-            auto f1 = [&](const char* n, float def, bool* found) {
-                const Param* p = shapeParams.floats(n);
-                if (!p) p = gs_.materialParams.floats(n);
-                if (found) *found = p && !p->nums.empty();
-                return (p && !p->nums.empty()) ? (float)p->nums[0] : def;
-            };
-            const float rough = f1("roughness", .01f, nullptr);
+            const float rough = f1("roughness", .01f, nullptr, shapeParams);
             bool hu = false, hv = false;
-            float ur = f1("uroughness", 0.f, &hu), vr = f1("vroughness", 0.f, &hv);
+            float ur = f1("uroughness", 0.f, &hu, shapeParams), vr = f1("vroughness", 0.f, &hv, shapeParams);
             if (!hu) ur = rough;
             if (!hv) vr = rough;
             bool remap = gs_.materialParams.bool1("remaproughness", true);
@@ -652,6 +663,57 @@ class Loader {
             for (int i = 0; i < 3; ++i) { m.eta[i] = eta[i]; m.k[i] = k[i]; }
             m.alpha[0] = std::max(0.001f, ur);  // TrowbridgeReitzDistribution ctor (microfacet.h:109-113)
             m.alpha[1] = std::max(0.001f, vr);
+        } else if (name == "glass" || name == "dispersive_glass") {
+            // CreateGlassMaterial (glass.cpp:85-100) / CreateDispersiveGlassMaterial
+            // (dispersive_glass.cpp:125-143)
+            const bool disp = name == "dispersive_glass";
+            m.kind = disp ? PT_MAT_DISPERSIVE_GLASS : PT_MAT_GLASS;
+            no_textures({"Kr", "Kt", "eta", "index", "etaMin", "etaMax", "indexMin", "indexMax", "uroughness",
+                         "vroughness", "bumpmap"}, shapeParams);
+            float kr[3] = {1, 1, 1}, kt[3] = {1, 1, 1};
+            spectrum2("Kr", kr, shapeParams);
+            spectrum2("Kt", kt, shapeParams);
+            bool found = false;
+            if (disp) {
+                m.ior_min = f1("etaMin", 0.f, &found, shapeParams);
+                if (!found) m.ior_min = f1("indexMin", 1.5f, nullptr, shapeParams);
+                m.ior_max = f1("etaMax", 0.f, &found, shapeParams);
+                if (!found) m.ior_max = f1("indexMax", 1.5f, nullptr, shapeParams);
+            } else {
+                m.ior = f1("eta", 0.f, &found, shapeParams);
+                if (!found) m.ior = f1("index", 1.5f, nullptr, shapeParams);
+            }
+            float ur = f1("uroughness", 0.f, nullptr, shapeParams), vr = f1("vroughness", 0.f, nullptr, shapeParams);
+            bool remap = gs_.materialParams.bool1("remaproughness", false);
+            remap = shapeParams.bool1("remaproughness", remap);
+            m.specular = (ur == 0 && vr == 0) ? 1 : 0;
+            if (remap) {
+                ur = tr_roughness_to_alpha(ur);
+                vr = tr_roughness_to_alpha(vr);
+            }
+            for (int i = 0; i < 3; ++i) { m.kr[i] = kr[i]; m.kt[i] = kt[i]; }
+            m.alpha[0] = std::max(0.001f, ur);
+            m.alpha[1] = std::max(0.001f, vr);
+        } else if (name == "mirror") {
+            // CreateMirrorMaterial (mirror.cpp:54-60)
+            m.kind = PT_MAT_MIRROR;
+            no_textures({"Kr", "bumpmap"}, shapeParams);
+            float kr[3] = {0.9f, 0.9f, 0.9f};
+            spectrum2("Kr", kr, shapeParams);
+            for (int i = 0; i < 3; ++i) m.kr[i] = kr[i];
+        } else if (name == "plastic") {
+            // CreatePlasticMaterial (plastic.cpp:72-83)
+            m.kind = PT_MAT_PLASTIC;
+            no_textures({"Kd", "Ks", "roughness", "bumpmap"}, shapeParams);
+            float kd[3] = {0.25f, 0.25f, 0.25f}, ks[3] = {0.25f, 0.25f, 0.25f};
+            spectrum2("Kd", kd, shapeParams);
+            spectrum2("Ks", ks, shapeParams);
+            float rough = f1("roughness", .1f, nullptr, shapeParams);
+            bool remap = gs_.materialParams.bool1("remaproughness", true);
+            remap = shapeParams.bool1("remaproughness", remap);
+            if (remap) rough = tr_roughness_to_alpha(rough);
+            for (int i = 0; i < 3; ++i) { m.kd[i] = kd[i]; m.ks[i] = ks[i]; }
+            m.alpha[0] = m.alpha[1] = std::max(0.001f, rough);
         } else {
             throw PtError(PT_ERR_UNSUPPORTED, "material \"" + name + "\" is outside the supported subset");
         }

@@ -280,12 +280,13 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     }
     for (int i = 0; i < d->n_materials; ++i) {
         int k = d->materials[i].kind;
-        if (k != PT_MAT_NONE && k != PT_MAT_MATTE && k != PT_MAT_METAL)
-            throw PtError(PT_ERR_UNSUPPORTED, "unsupported material kind");
+        if (k < PT_MAT_NONE || k > PT_MAT_PLASTIC) throw PtError(PT_ERR_UNSUPPORTED, "unsupported material kind");
         if (k == PT_MAT_MATTE && d->materials[i].sigma != 0.f)
             throw PtError(PT_ERR_UNSUPPORTED, "OrenNayar (sigma != 0) not supported");
-        if (k == PT_MAT_METAL && !(d->materials[i].alpha[0] > 0 && d->materials[i].alpha[1] > 0))
-            throw PtError(PT_ERR_INVALID_ARG, "metal alpha must be positive");
+        if ((k == PT_MAT_METAL || k == PT_MAT_PLASTIC ||
+             ((k == PT_MAT_GLASS || k == PT_MAT_DISPERSIVE_GLASS) && !d->materials[i].specular)) &&
+            !(d->materials[i].alpha[0] > 0 && d->materials[i].alpha[1] > 0))
+            throw PtError(PT_ERR_INVALID_ARG, "microfacet alpha must be positive");
     }
     for (int i = 0; i < d->n_lights; ++i) {
         const pt_light& l = d->lights[i];

@@ -102,7 +102,10 @@ def _fptr(a: np.ndarray):
 class pt_material(ctypes.Structure):
     """include/pt.h pt_material"""
     _fields_ = [("kind", ctypes.c_int32), ("kd", ctypes.c_float * 3), ("sigma", ctypes.c_float),
-                ("eta", ctypes.c_float * 3), ("k", ctypes.c_float * 3), ("alpha", ctypes.c_float * 2)]
+                ("eta", ctypes.c_float * 3), ("k", ctypes.c_float * 3), ("alpha", ctypes.c_float * 2),
+                ("ks", ctypes.c_float * 3), ("kr", ctypes.c_float * 3), ("kt", ctypes.c_float * 3),
+                ("ior", ctypes.c_float), ("ior_min", ctypes.c_float), ("ior_max", ctypes.c_float),
+                ("specular", ctypes.c_int32)]
 
 
 class _desc_prefix(ctypes.Structure):

@@ -233,3 +233,175 @@ def test_plymesh_bad_index_is_an_error(tmp_path):
     with pytest.raises(ptgpu.PtError) as e:
         ptgpu.HostScene(scene_variant(tmp_path, extra=[("WorldEnd", extra)]))
     assert e.value.status == 2  # PT_ERR_PARSE
+
+
+# ---- dielectrics, plastic, mirror (glass.cpp, dispersive_glass.cpp, plastic.cpp, mirror.cpp) ---------
+
+def material_scene(tmp_path, material, **kw):
+    box = ('AttributeBegin\n  %s\n  Shape "trianglemesh" "point P" [150 0 150  400 0 150  400 200 300  150 200 300] '
+           '"integer indices" [0 1 2 0 2 3]\nAttributeEnd\n' % material)
+    return scene_variant(tmp_path, extra=[("WorldEnd", box + "WorldEnd")], **kw)
+
+
+def _index_of(hs, kind):
+    return [i for i, m in enumerate(hs.materials()) if m.kind == kind][0]
+
+
+def test_material_parameters(tmp_path):
+    hs = ptgpu.HostScene(material_scene(tmp_path, 'Material "glass" "float index" [1.33] "rgb Kt" [0.9 0.8 0.7] '
+                                                  '"float uroughness" [0.2] "float vroughness" [0.1]'))
+    m = hs.materials()[_index_of(hs, 3)]
+    assert F32(m.ior) == F32(1.33) and m.specular == 0 and list(m.kr) == [1, 1, 1]
+    assert list(m.alpha) == [F32(0.2), F32(0.1)]       # glass: remaproughness defaults to false
+    hs = ptgpu.HostScene(material_scene(tmp_path, 'Material "plastic" "rgb Kd" [0.1 0.2 0.3]'))
+    m = hs.materials()[_index_of(hs, 6)]
+    assert list(m.ks) == [F32(0.25)] * 3 and m.alpha[0] == max(F32(0.001), roughness_to_alpha(0.1))
+    hs = ptgpu.HostScene(material_scene(tmp_path, 'Material "dispersive_glass" "float etaMin" [1.22] '
+                                                  '"float etaMax" [1.38]'))
+    m = hs.materials()[_index_of(hs, 4)]
+    assert (F32(m.ior_min), F32(m.ior_max), m.specular) == (F32(1.22), F32(1.38), 1)
+    hs = ptgpu.HostScene(material_scene(tmp_path, 'Material "mirror"'))
+    assert list(hs.materials()[_index_of(hs, 5)].kr) == [F32(0.9)] * 3
+
+
+def _chi2_sphere(desc, mat, wo, n, rng, theta_res=10, phi_res=20, k=10, ior=None):
+    """Chi^2 of BSDF::Sample_f against BSDF::Pdf over the whole sphere
+    (the bsdfs.cpp procedure; reflection and transmission cells).
+
+    MicrofacetTransmission::Pdf (reflection.cpp:479-493) weights the half
+    vector with AbsDot(wo, wh), so it also assigns density to refraction
+    directions whose microfacet faces away from wo, which visible-normal
+    sampling never produces (the reference's own chi^2 tests cover reflection
+    BxDFs only).  With `ior`, the expected table leaves those out."""
+    from scipy.stats import chi2
+    rec = np.zeros((n, 8), np.float32)
+    rec[:, 0:3] = wo
+    rec[:, 6:8] = rng.random((n, 2), dtype=np.float32) * F32(0.99999994)
+    out = pyoracle.bsdf_batch(desc, mat, rec)
+    ok = (out[:, 0:3].max(axis=1) > 0) & (out[:, 7] > 0)
+    wi = out[ok, 4:7].astype(np.float64)
+    th = np.arccos(np.clip(wi[:, 2], -1, 1)) * theta_res / math.pi
+    ph = np.arctan2(wi[:, 1], wi[:, 0])
+    ph = np.where(ph < 0, ph + 2 * math.pi, ph) * phi_res / (2 * math.pi)
+    ti = np.clip(np.floor(th).astype(int), 0, theta_res - 1)
+    pi_ = np.clip(np.floor(ph).astype(int), 0, phi_res - 1)
+    obs = np.bincount(ti * phi_res + pi_, minlength=theta_res * phi_res).astype(np.float64)
+    tt = (np.arange(theta_res * k) + 0.5) * math.pi / (theta_res * k)
+    pp = (np.arange(phi_res * k) + 0.5) * 2 * math.pi / (phi_res * k)
+    T, P = np.meshgrid(tt, pp, indexing="ij")
+    dirs = np.stack([np.sin(T) * np.cos(P), np.sin(T) * np.sin(P), np.cos(T)], -1).reshape(-1, 3)
+    q = np.zeros((len(dirs), 8), np.float32)
+    q[:, 0:3] = wo
+    q[:, 3:6] = dirs
+    pdf = pyoracle.bsdf_batch(desc, mat, q)[:, 3].astype(np.float64)
+    if ior is not None:
+        wo64 = wo.astype(np.float64)
+        trans = dirs[:, 2] * wo64[2] < 0
+        eta = ior if wo64[2] > 0 else 1.0 / ior
+        whp = wo64 + dirs * eta
+        whp /= np.linalg.norm(whp, axis=1, keepdims=True)
+        whs = np.where((whp[:, 2] * wo64[2] > 0)[:, None], whp, -whp)
+        pdf = np.where(trans & (whs @ wo64 <= 0), 0.0, pdf)
+    pdf = pdf.reshape(theta_res * k, phi_res * k)
+    cell = (math.pi / (theta_res * k)) * (2 * math.pi / (phi_res * k))
+    exp = (pdf * np.sin(T) * cell).reshape(theta_res, k, phi_res, k).sum(axis=(1, 3)).reshape(-1) * n
+    order = np.argsort(exp)
+    stat, dof, pool_o, pool_e = 0.0, 0, 0.0, 0.0
+    for i in order:
+        if exp[i] < 5:
+            pool_o += obs[i]
+            pool_e += exp[i]
+            continue
+        stat += (obs[i] - exp[i]) ** 2 / exp[i]
+        dof += 1
+    if pool_e >= 5:
+        stat += (pool_o - pool_e) ** 2 / pool_e
+        dof += 1
+    return 1.0 - chi2.cdf(stat, dof - 1)
+
+
+@pytest.mark.parametrize("material,n", [
+    ('Material "glass" "float index" [1.5] "float uroughness" [0.3] "float vroughness" [0.3]', 300000),
+    # anisotropic refraction: TrowbridgeReitzSample11 samples slope_y through a
+    # rational-polynomial fit of the inverse CDF (microfacet.cpp:270-275), and the
+    # refraction Jacobian magnifies its ~1e-3 deviation from Pdf, which 300k
+    # samples resolve; 60k do not (the reference's own TR_VA tests are
+    # reflection-only at 1M samples)
+    ('Material "glass" "float index" [1.33] "float uroughness" [0.4] "float vroughness" [0.15] "rgb Kr" [0.5 0.5 0.5]',
+     60000),
+    ('Material "plastic" "rgb Kd" [0.4 0.3 0.2] "rgb Ks" [0.5 0.5 0.5] "float roughness" [0.1]', 300000)])
+def test_multilobe_sampling_chi2(tmp_path, material, n):
+    """Two-lobe BSDFs (MicrofacetReflection + MicrofacetTransmission, Lambertian
+    + MicrofacetReflection): component choice, pdf averaging and each lobe's
+    sampling agree with BSDF::Pdf (bsdfs.cpp chi^2 procedure)."""
+    hs = ptgpu.HostScene(material_scene(tmp_path, material, res=(8, 8), spp=1))
+    mat = [i for i, m in enumerate(hs.materials()) if m.kind in (3, 6)][0]
+    ior = float(hs.materials()[mat].ior) if hs.materials()[mat].kind == 3 else None
+    rng = np.random.default_rng(3)
+    runs = 3
+    sig = 1.0 - (1.0 - 0.01) ** (1.0 / runs)
+    for run in range(runs):
+        wo = _cosine_hemisphere(*rng.random(2))
+        if run == 1:
+            wo[2] = -wo[2]                       # from inside the dielectric
+        pval = _chi2_sphere(hs.desc, mat, wo.astype(np.float32), n, rng, ior=ior)
+        assert pval > sig, (run, pval)
+
+
+def test_specular_dielectric_energy(tmp_path):
+    """FresnelSpecular: reflection + transmission probabilities sum to one and the
+    sampled weights f |cos| / pdf equal R (reflection) or T (eta_i/eta_t)^2
+    (transmission, TransportMode::Radiance)."""
+    hs = ptgpu.HostScene(material_scene(tmp_path, 'Material "glass" "float index" [1.5]'))
+    mat = _index_of(hs, 3)
+    rng = np.random.default_rng(5)
+    n = 20000
+    wo = rng.normal(size=(n, 3))
+    wo /= np.linalg.norm(wo, axis=1, keepdims=True)
+    rec = np.zeros((n, 8), np.float32)
+    rec[:, 0:3] = wo
+    rec[:, 6:8] = rng.random((n, 2)) * 0.99999994
+    out = pyoracle.bsdf_batch(hs.desc, mat, rec).astype(np.float64)
+    wi, f, pdf = out[:, 4:7], out[:, 0:3], out[:, 7]
+    good = pdf > 0
+    w = f[good, 0] * np.abs(wi[good, 2]) / pdf[good]
+    refl = (wi[good, 2] * wo[good, 2]) > 0
+    np.testing.assert_allclose(w[refl], 1.0, rtol=1e-5)
+    entering = wo[good, 2][~refl] > 0
+    expect = np.where(entering, (1 / 1.5) ** 2, 1.5 ** 2)
+    np.testing.assert_allclose(w[~refl], expect, rtol=1e-5)
+
+
+@pytest.mark.parametrize("glass", ['Material "glass" "float index" [1.5]',
+                                   'Material "dispersive_glass" "float etaMin" [1.3] "float etaMax" [1.6]',
+                                   'Material "glass" "float index" [1.4] "float uroughness" [0.2] '
+                                   '"float vroughness" [0.2]'])
+@pytest.mark.parametrize("z0,z1,expect", [(0.2, 0.7, 1.0), (-0.3, 0.3, 2.25)])
+def test_furnace_with_dielectric(tmp_path, glass, z0, z1, expect):
+    """A lossless dielectric block inside the Kd = 0.5, Le = 0.5 furnace
+    (analytic_scenes.cpp:135-165: radiance 1).  In front of the camera it
+    leaves the radiance at 1 (FresnelSpecular / microfacet transmission
+    conserve energy up to the single-scattering loss of rough interfaces; the
+    eta^2 radiance scaling cancels on the way out); with
+    the camera inside an index-1.5 block the radiance is eta^2 = 2.25 times
+    higher (TransportMode::Radiance, reflection.cpp:547-548)."""
+    from conftest import furnace_scene
+    if expect != 1.0 and "1.5" not in glass:
+        pytest.skip("eta^2 check is for the index-1.5 glass")
+    p = furnace_scene(tmp_path, res=10, spp=256, maxdepth=40)
+    pts = [(x, y, z) for z in (z0, z1) for (x, y) in ((-0.4, -0.4), (0.4, -0.4), (0.4, 0.4), (-0.4, 0.4))]
+    # outward-facing: Triangle normal = Cross(p0 - p2, p1 - p2) (triangle.cpp:347)
+    idx = "0 2 1 0 3 2  4 5 6 4 6 7  0 1 5 0 5 4  3 7 6 3 6 2  0 4 7 0 7 3  1 2 6 1 6 5"
+    block = ('AttributeBegin\n  %s\n  Shape "trianglemesh" "point P" [%s] "integer indices" [%s]\nAttributeEnd\n' %
+             (glass, " ".join("%g %g %g" % q for q in pts), idx))
+    txt = open(p).read().replace("WorldEnd", block + "WorldEnd")
+    open(p, "w").write(txt)
+    hs = ptgpu.HostScene(p)
+    img, _ = pyoracle.render(hs.desc, nthreads=8)
+    mean = float(img.mean())
+    if "roughness" in glass:
+        # single-scattering microfacet BTDF/BRDF lose the energy of
+        # inter-microfacet bounces (alpha = RoughnessToAlpha(0.2) = 0.68 here)
+        assert 0.85 < mean < 1.0 + 0.03, mean
+    else:
+        assert abs(mean - expect) < 0.03 * expect, mean
