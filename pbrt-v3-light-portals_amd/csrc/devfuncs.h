@@ -442,6 +442,24 @@ constexpr int kBxR = 1, kBxT = 2, kBxDiffuse = 4, kBxGlossy = 8, kBxSpecular = 1
 constexpr int kBxNonSpecular = kBxAll & ~kBxSpecular;
 enum LobeKind { kLbLambert = 1, kLbMfRefl = 2, kLbMfTrans = 3, kLbFresnelSpec = 4, kLbSpecRefl = 5 };
 
+// Scene features the shading code is compiled for (template argument kFt).
+// The host picks the smallest instantiation covering the scene (render.hip,
+// scene_features); code for absent materials / lights is compiled out, which
+// cuts the shading kernel's register pressure for the all-matte scenes.
+enum : int {
+    kFtMicro = 1,       // metal, plastic, rough glass: microfacet lobes, two-lobe BSDFs
+    kFtSpecular = 2,    // smooth glass, dispersive glass, mirror: specular lobes
+    kFtInfinite = 4,    // an InfiniteAreaLight
+    kFtAll = 7
+};
+template <int kFt>
+struct Ft {
+    static constexpr bool micro = (kFt & kFtMicro) != 0;
+    static constexpr bool spec = (kFt & kFtSpecular) != 0;
+    static constexpr bool inf = (kFt & kFtInfinite) != 0;
+    static constexpr int max_lobes = micro ? 2 : 1;
+};
+
 __device__ __forceinline__ int lobe_type(int k) {
     switch (k) {
         case kLbLambert: return kBxR | kBxDiffuse;
@@ -545,14 +563,16 @@ __device__ __forceinline__ float mftrans_pdf(const Bsdf& b, V3 wo, V3 wi) {
 }
 __device__ __forceinline__ S3 lambert_R(const Bsdf& b) { return clamp0(s3(b.m->kd[0], b.m->kd[1], b.m->kd[2])); }
 
+template <int kFt = kFtAll>
 __device__ __forceinline__ S3 lobe_f(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::f
-    if (k == kLbLambert) return lambert_R(b) * kInvPi;
+    if (!Ft<kFt>::micro || k == kLbLambert) return lambert_R(b) * kInvPi;
     if (k == kLbMfRefl) return mfrefl_f(b, wo, wi);
     if (k == kLbMfTrans) return mftrans_f(b, wo, wi);
     return s3(0.f);
 }
+template <int kFt = kFtAll>
 __device__ __forceinline__ float lobe_pdf(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::Pdf
-    if (k == kLbLambert) return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    if (!Ft<kFt>::micro || k == kLbLambert) return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
     if (k == kLbMfRefl) {
         if (!(wo.z * wi.z > 0)) return 0.f;
         const V3 wh = normalize(wo + wi);
@@ -561,17 +581,19 @@ __device__ __forceinline__ float lobe_pdf(const Bsdf& b, int k, V3 wo, V3 wi) { 
     if (k == kLbMfTrans) return mftrans_pdf(b, wo, wi);
     return 0.f;
 }
-// BxDF::Sample_f; *type narrowed by FresnelSpecular
+// BxDF::Sample_f; *type narrowed by FresnelSpecular.  Non-specular lobes only
+// when the scene has no specular materials (kFt without kFtSpecular).
+template <int kFt = kFtAll>
 __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, float u0, float u1, float* pdf,
                                           int* type) {
     const pt_material* m = b.m;
-    if (k == kLbLambert) {
+    if (k == kLbLambert || !(Ft<kFt>::micro || Ft<kFt>::spec)) {
         *wi = cosine_sample_hemisphere(u0, u1);
         if (wo.z < 0) wi->z *= -1;
-        *pdf = lobe_pdf(b, k, wo, *wi);
-        return lobe_f(b, k, wo, *wi);
+        *pdf = lobe_pdf<kFt>(b, kLbLambert, wo, *wi);
+        return lobe_f<kFt>(b, kLbLambert, wo, *wi);
     }
-    if (k == kLbMfRefl || k == kLbMfTrans) {
+    if (Ft<kFt>::micro && (k == kLbMfRefl || k == kLbMfTrans || !Ft<kFt>::spec)) {
         const float ax = m->alpha[0], ay = m->alpha[1];
         if (wo.z == 0) return s3(0.f);
         const V3 wh = tr_sample_wh(ax, ay, wo, u0, u1);
@@ -587,6 +609,7 @@ __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, f
         *pdf = mftrans_pdf(b, wo, *wi);
         return mftrans_f(b, wo, *wi);
     }
+    if (!Ft<kFt>::spec) return s3(0.f);
     if (k == kLbSpecRefl) {  // SpecularReflection::Sample_f, FresnelNoOp
         *wi = refl_z(wo);
         *pdf = 1;
@@ -619,6 +642,7 @@ __device__ __forceinline__ void add_lobe(Bsdf* b, int k) {
 }
 // Material::ComputeScatteringFunctions(..., Radiance, allowMultipleLobes = true)
 // + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength.
+template <int kFt = kFtAll>
 __device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, float wvl0, Bsdf* b) {
     b->ns = si.sn;
     b->ng = si.n;
@@ -629,13 +653,13 @@ __device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& s
     b->lk0 = b->lk1 = 0;
     b->eta = 1;
     const int kind = m->kind;
-    if (kind == PT_MAT_MATTE) {
+    if (kind == PT_MAT_MATTE || !(Ft<kFt>::micro || Ft<kFt>::spec)) {
         if (!is_black(lambert_R(*b))) add_lobe(b, kLbLambert);
-    } else if (kind == PT_MAT_METAL) {
+    } else if (Ft<kFt>::micro && kind == PT_MAT_METAL) {
         add_lobe(b, kLbMfRefl);
-    } else if (kind == PT_MAT_MIRROR) {
+    } else if (Ft<kFt>::spec && kind == PT_MAT_MIRROR) {
         if (!is_black(clamp0(s3(m->kr[0], m->kr[1], m->kr[2])))) add_lobe(b, kLbSpecRefl);
-    } else if (kind == PT_MAT_PLASTIC) {
+    } else if (Ft<kFt>::micro && kind == PT_MAT_PLASTIC) {
         if (!is_black(lambert_R(*b))) add_lobe(b, kLbLambert);
         if (!is_black(clamp0(s3(m->ks[0], m->ks[1], m->ks[2])))) add_lobe(b, kLbMfRefl);
     } else if (kind == PT_MAT_GLASS || kind == PT_MAT_DISPERSIVE_GLASS) {
@@ -650,9 +674,9 @@ __device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& s
         const bool hasR = !is_black(clamp0(s3(m->kr[0], m->kr[1], m->kr[2])));
         const bool hasT = !is_black(clamp0(s3(m->kt[0], m->kt[1], m->kt[2])));
         if (!hasR && !hasT) return;
-        if (m->specular) {
+        if (Ft<kFt>::spec && (m->specular || !Ft<kFt>::micro)) {
             add_lobe(b, kLbFresnelSpec);
-        } else {
+        } else if (Ft<kFt>::micro) {
             if (hasR) add_lobe(b, kLbMfRefl);
             if (hasT) add_lobe(b, kLbMfTrans);
         }
@@ -665,47 +689,52 @@ __device__ __forceinline__ V3 l2w(const Bsdf& b, V3 v) {
               b.ss.z * v.x + b.ts.z * v.y + b.ns.z * v.z);
 }
 __device__ __forceinline__ bool lobe_matches(int k, int flags) { return (lobe_type(k) & flags) == lobe_type(k); }
+template <int kFt = kFtAll>
 __device__ __forceinline__ int bsdf_num(const Bsdf& b, int flags) {  // BSDF::NumComponents
     int n = 0;
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < Ft<kFt>::max_lobes; ++i)
         if (i < b.n) n += lobe_matches(lobe_at(b, i), flags) ? 1 : 0;
     return n;
 }
+template <int kFt = kFtAll>
 __device__ __forceinline__ S3 bsdf_f(const Bsdf& b, V3 woW, V3 wiW, int flags) {  // reflection.cpp:713-726
     const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return s3(0.f);
     const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
     S3 f = s3(0.f);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
         if (i >= b.n) break;
         const int k = lobe_at(b, i), t = lobe_type(k);
-        if (lobe_matches(k, flags) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT)))) f = f + lobe_f(b, k, wo, wi);
+        if (lobe_matches(k, flags) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT))))
+            f = f + lobe_f<kFt>(b, k, wo, wi);
     }
     return f;
 }
+template <int kFt = kFtAll>
 __device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW, int flags) {  // reflection.cpp:814-829
     if (b.n == 0) return 0.f;
     const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return 0.f;
     float pdf = 0.f;
     int matching = 0;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
         if (i >= b.n) break;
         const int k = lobe_at(b, i);
-        if (lobe_matches(k, flags)) { ++matching; pdf += lobe_pdf(b, k, wo, wi); }
+        if (lobe_matches(k, flags)) { ++matching; pdf += lobe_pdf<kFt>(b, k, wo, wi); }
     }
     return matching > 0 ? pdf / matching : 0.f;
 }
 // BSDF::Sample_f (reflection.cpp:747-812); *pdf stays 0 wherever the reference
 // returns black before writing it; *sampled is the sampled BxDFType.
+template <int kFt = kFtAll>
 __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf, int flags,
                                           int* sampled) {
-    const int matchingComps = bsdf_num(b, flags);
+    const int matchingComps = bsdf_num<kFt>(b, flags);
     if (matchingComps == 0) { *pdf = 0; *sampled = 0; return s3(0.f); }
     int comp = (int)floorf(u0 * matchingComps);
     comp = comp < matchingComps - 1 ? comp : matchingComps - 1;
     int bk = b.lk0, count = comp;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
         if (i >= b.n) break;
         if (lobe_matches(lobe_at(b, i), flags) && count-- == 0) { bk = lobe_at(b, i); break; }
     }
@@ -715,25 +744,25 @@ __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float 
     *pdf = 0;
     *sampled = lobe_type(bk);
     V3 wi = v3(0, 0, 0);
-    S3 f = lobe_sample(b, bk, wo, &wi, ur0, u1, pdf, sampled);
+    S3 f = lobe_sample<kFt>(b, bk, wo, &wi, ur0, u1, pdf, sampled);
     if (*pdf == 0) { *sampled = 0; return s3(0.f); }
     *wiW = l2w(b, wi);
     const bool spec = (lobe_type(bk) & kBxSpecular) != 0;
     if (!spec && matchingComps > 1)
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
             if (i >= b.n) break;
             const int k = lobe_at(b, i);
-            if (k != bk && lobe_matches(k, flags)) *pdf += lobe_pdf(b, k, wo, wi);
+            if (k != bk && lobe_matches(k, flags)) *pdf += lobe_pdf<kFt>(b, k, wo, wi);
         }
     if (matchingComps > 1) *pdf /= matchingComps;
     if (!spec) {
         const bool reflect = dot(*wiW, b.ng) * dot(woW, b.ng) > 0;
         f = s3(0.f);
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
             if (i >= b.n) break;
             const int k = lobe_at(b, i), t = lobe_type(k);
             if (lobe_matches(k, flags) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT))))
-                f = f + lobe_f(b, k, wo, wi);
+                f = f + lobe_f<kFt>(b, k, wo, wi);
         }
     }
     return f;
@@ -853,10 +882,11 @@ __device__ __forceinline__ float inf_pdf_li(const DevLight& l, V3 w) {
 }
 
 // DiffuseAreaLight::Sample_Li + Shape::Sample(ref, u, pdf) (diffuse.cpp:69-84, shape.cpp:56-74)
+template <int kFt = kFtAll>
 __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, float u0,
                                              float u1, V3* wi, float* pdf, V3* sp, V3* sn, V3* spe) {
     V3 p, n, pe;
-    if (l.kind == PT_LIGHT_INFINITE) {
+    if (Ft<kFt>::inf && l.kind == PT_LIGHT_INFINITE) {
         *sn = v3(0, 0, 0);
         *spe = v3(0, 0, 0);
         return inf_sample_li(l, ref.p, u0, u1, wi, pdf, sp);
@@ -877,8 +907,9 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
 }
 
 // Shape::Pdf(ref, wi) for the light's shape (shape.cpp:76-91)
+template <int kFt = kFtAll>
 __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, V3 wi) {
-    if (l.kind == PT_LIGHT_INFINITE) return inf_pdf_li(l, wi);
+    if (Ft<kFt>::inf && l.kind == PT_LIGHT_INFINITE) return inf_pdf_li(l, wi);
     Ray r{offset_ray_origin(ref.p, ref.perr, ref.n, wi), wi, kInf};
     SurfHit isl;
     bool ok;

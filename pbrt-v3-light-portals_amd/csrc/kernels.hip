@@ -608,6 +608,7 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 
 // Finish the NEE of the previous vertex: Ld from the traced rays, then
 // L += beta * Ld / lightPdf (integrator.cpp:121, path.cpp:122-127).
+template <int kFt>
 __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, S3* L) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
@@ -636,7 +637,7 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
                 int lid;
                 const S3 le = hit_Le(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
                 if (lid == nl) Li = le;
-            } else if (sc.lights[nl].kind == PT_LIGHT_INFINITE) {
+            } else if (Ft<kFt>::inf && sc.lights[nl].kind == PT_LIGHT_INFINITE) {
                 Li = inf_Le(sc.lights[nl], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
             }
             if (!is_black(Li)) {
@@ -659,6 +660,7 @@ __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int 
 // PortalArealight::EstimateDirect set-up (portal_arealight.cpp:29-239).
 // u1 = uScattering (argument order at integrator.cpp:132); u2 is unused; the
 // selected portal is call-local.  Returns true when ray A was emitted.
+template <int kFt>
 __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                            const SurfHit& it, const Bsdf& bsdf, float u10, float u11) {
     const DevLight& l = sc.lights[lightIdx];
@@ -733,7 +735,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                 if (pdf > 0) {
                     const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
                     store_ray6(ps.rayA, N, slot, r);
-                    put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
+                    put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
                     put_nee(ps, slot, kNeePdf, pdf);
                     put_nee3(ps, slot, kNeeLi, s3(0.f));
                     flags |= kNfA;
@@ -746,11 +748,11 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
     // EstimateDirectLight (portal_arealight.cpp:115-156)
     V3 wi, sp, sn, spe;
     float pdf = 0;
-    const S3 Li = area_sample_li(sc, l, it, u10, u11, &wi, &pdf, &sp, &sn, &spe);
+    const S3 Li = area_sample_li<kFt>(sc, l, it, u10, u11, &wi, &pdf, &sp, &sn, &spe);
     if (!is_black(Li) && pdf > 0) {
         const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
         store_ray6(ps.rayA, N, slot, r);
-        put_nee3(ps, slot, kNeeF, bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
+        put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
         put_nee(ps, slot, kNeePdf, pdf);
         put_nee3(ps, slot, kNeeLi, Li);
         flags |= kNfA;
@@ -761,6 +763,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
 
 // EstimateDirect, MIS branch (integrator.cpp:137-258) for a DiffuseAreaLight.
 // Emits ray A (shadow, any-hit) and/or ray B (BSDF-sampled, closest-hit).
+template <int kFt>
 __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                             const SurfHit& it, const Bsdf& bsdf, float ul0, float ul1, float us0,
                                             float us1) {
@@ -769,10 +772,10 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
     uint32_t flags = kNfMis;
     V3 wi, sp, sn, spe;
     float lightPdf = 0, scatteringPdf = 0;
-    const S3 Li = area_sample_li(sc, l, it, ul0, ul1, &wi, &lightPdf, &sp, &sn, &spe);
+    const S3 Li = area_sample_li<kFt>(sc, l, it, ul0, ul1, &wi, &lightPdf, &sp, &sn, &spe);
     if (lightPdf > 0 && !is_black(Li)) {
-        const S3 f = bsdf_f(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn);
-        scatteringPdf = bsdf_pdf(bsdf, it.wo, wi, kBxNonSpecular);
+        const S3 f = bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn);
+        scatteringPdf = bsdf_pdf<kFt>(bsdf, it.wo, wi, kBxNonSpecular);
         if (!is_black(f)) {
             // VisibilityTester::Unoccluded -> SpawnRayTo(Interaction) (light.cpp:59-61, interaction.h:75-80)
             const V3 origin = offset_ray_origin(it.p, it.perr, it.n, sp - it.p);
@@ -791,10 +794,10 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
         float pdf2 = scatteringPdf;
         V3 wi2 = wi;
         int sampledType = 0;
-        S3 f = bsdf_sample(bsdf, it.wo, &wi2, us0, us1, &pdf2, kBxNonSpecular, &sampledType);
+        S3 f = bsdf_sample<kFt>(bsdf, it.wo, &wi2, us0, us1, &pdf2, kBxNonSpecular, &sampledType);
         f = f * absdot(wi2, it.sn);
         if (!is_black(f) && pdf2 > 0) {
-            const float lp = area_pdf_li(sc, l, it, wi2);
+            const float lp = area_pdf_li<kFt>(sc, l, it, wi2);
             if (lp != 0) {
                 const float sw = power_heuristic(pdf2, lp);
                 const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi2), wi2, kInf};
@@ -813,6 +816,7 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
 
 // One path step.  Returns the rays to enqueue in rays[] and whether the path
 // stays alive.
+template <int kFt>
 __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
                                            uint32_t* nrays, bool* keep, bool* overflow) {
     const uint32_t N = (uint32_t)ps.n;
@@ -820,7 +824,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
     S3 L = load_s3(ps.L, N, slot);
     *nrays = 0;
     if (st & kStNee) {
-        resolve_nee(sc, ps, slot, &L);
+        resolve_nee<kFt>(sc, ps, slot, &L);
         st &= ~kStNee;
     }
     if (st & kStCont) {
@@ -836,7 +840,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         if (found) prim_info(sc, hp, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
-            else
+            else if (Ft<kFt>::inf)
                 for (int li = 0; li < sc.n_lights; ++li)  // scene.infiniteLights, in light order
                     if (sc.lights[li].kind == PT_LIGHT_INFINITE) L = L + beta * inf_Le(sc.lights[li], ray.d);
         }
@@ -851,10 +855,10 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
-                const float wvl0 = sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
+                const float wvl0 = Ft<kFt>::spec && sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
                                        ? (float)400 + (float)300 * halton_dim(sc, dm.idx, 5) : 550.f;
-                make_bsdf(&sc.mats[mat], si, wvl0, &bsdf);
-                if (bsdf_num(bsdf, kBxNonSpecular) > 0) {
+                make_bsdf<kFt>(&sc.mats[mat], si, wvl0, &bsdf);
+                if (bsdf_num<kFt>(bsdf, kBxNonSpecular) > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
                     bool deferred = false;
                     float lightPdf = 0;
@@ -868,12 +872,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                             const float uL0 = dm.get1(), uL1 = dm.get1();
                             const float uS0 = dm.get1(), uS1 = dm.get1();
                             if (sc.lights[ln].kind == PT_LIGHT_PORTAL_AREA) {
-                                if (portal_nee(sc, ps, slot, ln, si, bsdf, uS0, uS1)) {
+                                if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1)) {
                                     rays[(*nrays)++] = slot << 2 | kRayA;
                                     deferred = true;
                                 }
                             } else {
-                                const uint32_t f = mis_nee(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1);
+                                const uint32_t f = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1);
                                 if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
                                 if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
                                 deferred = (f & (kNfA | kNfB)) != 0;
@@ -894,12 +898,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 V3 wi = v3(0, 0, 0);
                 float pdf = 0;
                 int sampled = 0;
-                const S3 f = bsdf_sample(bsdf, -ray.d, &wi, u0, u1, &pdf, kBxAll, &sampled);
+                const S3 f = bsdf_sample<kFt>(bsdf, -ray.d, &wi, u0, u1, &pdf, kBxAll, &sampled);
                 if (!(is_black(f) || pdf == 0.f)) {
                     beta = beta * ((f * absdot(wi, si.sn)) / pdf);
                     if (sampled & kBxSpecular) st |= kStSpecular;
                     else st &= ~kStSpecular;
-                    if ((sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
+                    if (Ft<kFt>::spec && (sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
                         const float eta = bsdf.eta;
                         ps.eta[slot] *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
                     }
@@ -931,6 +935,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
     *keep = (st & (kStCont | kStNee)) != 0;
 }
 
+template <int kFt>
 __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
@@ -945,7 +950,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         uint32_t slot = 0;
         if (i < n) {
             slot = pq[i];
-            shade_path(sc, ps, slot, rays, &nrays, &keep, &overflow);
+            shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
         }
         const uint32_t pos = wave_reserve(rq_out_count, nrays);
         for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
@@ -955,23 +960,27 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
 
-// Register-budget variants of the shading kernel (occupancy vs spills);
-// render.hip picks one (PT_SHADE_VARIANT).
+// Register-budget variants of the shading kernel (occupancy vs spills), each
+// compiled for a scene-feature set kFt; render.hip picks one (PT_SHADE_VARIANT,
+// scene_features).
+template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
                                                        const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                                        uint32_t* rq_out_count, uint32_t* pq_out,
                                                        uint32_t* pq_out_count, DevStats* stats) {
-    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
+template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
-    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
+template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_w4(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
-    shade_batch(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 
 // ----------------------------------------------------------------------------

@@ -196,6 +196,7 @@ struct pt_scene {
     size_t target_slots = (size_t)8 << 20;
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
+    int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int refill_min = 64;         // idle lanes that trigger a refill (64: whole-wave refill)
@@ -207,6 +208,41 @@ struct pt_scene {
 namespace pt {
 
 static int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Smallest shading-kernel feature set (devfuncs.h kFt*) covering the scene's
+// materials and lights.  PT_SHADE_FEATURES overrides it (a superset renders the
+// same image: the extra code is simply unreachable).
+static int scene_features(const pt_scene_desc* d) {
+    int f = 0;
+    for (int i = 0; i < d->n_materials; ++i) {
+        const pt_material& m = d->materials[i];
+        if (m.kind == PT_MAT_METAL || m.kind == PT_MAT_PLASTIC) f |= kFtMicro;
+        if (m.kind == PT_MAT_MIRROR) f |= kFtSpecular;
+        if (m.kind == PT_MAT_GLASS || m.kind == PT_MAT_DISPERSIVE_GLASS) f |= m.specular ? kFtSpecular : kFtMicro;
+    }
+    for (int i = 0; i < d->n_lights; ++i)
+        if (d->lights[i].kind == PT_LIGHT_INFINITE) f |= kFtInfinite;
+    return f;
+}
+
+using ShadeKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                             uint32_t*, DevStats*);
+template <int kFt>
+static ShadeKernel shade_kernel_ft(int variant) {
+    return variant == 4 ? k_shade_w4<kFt> : (variant == 3 ? k_shade_w3<kFt> : k_shade<kFt>);
+}
+static ShadeKernel shade_kernel(int variant, int features) {
+    switch (features & kFtAll) {
+        case 0: return shade_kernel_ft<0>(variant);
+        case 1: return shade_kernel_ft<1>(variant);
+        case 2: return shade_kernel_ft<2>(variant);
+        case 3: return shade_kernel_ft<3>(variant);
+        case 4: return shade_kernel_ft<4>(variant);
+        case 5: return shade_kernel_ft<5>(variant);
+        case 6: return shade_kernel_ft<6>(variant);
+        default: return shade_kernel_ft<7>(variant);
+    }
+}
 
 // InfiniteAreaLight ctor + Preprocess (infinite.cpp:43-83): LightToWorld,
 // world bounding sphere of the BVH root, and the Distribution2D over the 2x2
@@ -747,7 +783,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     rr.launches++;
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
-                auto kshade = s->shade_variant == 4 ? k_shade_w4 : (s->shade_variant == 3 ? k_shade_w3 : k_shade);
+                const ShadeKernel kshade = shade_kernel(s->shade_variant, s->features);
                 hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out,
                                    counts + 2, pq_out, counts + 3, w.stats.p);
                 HIPCHK(hipGetLastError());
@@ -944,6 +980,8 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                  ? scene_bytes : 0;
         const char* v = std::getenv("PT_SHADE_VARIANT");
         if (v) s->shade_variant = std::atoi(v);
+        s->features = scene_features(desc);
+        if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
         if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
         if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
