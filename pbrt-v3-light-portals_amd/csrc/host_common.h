@@ -66,6 +66,10 @@ struct PlyMesh {
     bool hasN = false, hasUV = false;
 };
 void read_ply(const std::string& path, PlyMesh* out);
+// Shape "loopsubdiv" (shapes/loopsubdiv.cpp:137-398): refined limit-surface
+// mesh in object space -- positions, shading normals, triangle indices.
+void loop_subdivide(int levels, const std::vector<int>& indices, const std::vector<float>& P,
+                    std::vector<float>* outP, std::vector<float>* outN, std::vector<int>* outIdx);
 
 // SAH BVH build over the scene's primitives (bvh.cpp:190-402, 640-658).
 // prim_order[i] = index into desc->prims of the i-th primitive in BVH order.

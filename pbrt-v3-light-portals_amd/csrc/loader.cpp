@@ -772,6 +772,9 @@ class Loader {
         }
     }
 
+    // Error()/Warning() (error.cpp:89-102): print and continue
+    static void warn(const std::string& msg) { std::fprintf(stderr, "Error: %s\n", msg.c_str()); }
+
     void shape(const std::string& name, const ParamSet& ps) {
         if (!inWorld_) throw PtError(PT_ERR_PARSE, "Shape outside WorldBegin");
         const HXF o2w = ctm_;
@@ -812,6 +815,21 @@ class Loader {
                 idx = std::move(m.idx);
             }
             add_mesh(ps, oflags, P, N, S, UV, idx);
+        } else if (name == "loopsubdiv") {
+            // CreateLoopSubdiv (loopsubdiv.cpp:400-437): missing data is an
+            // Error() that yields no shapes; the mesh carries P and N only
+            const int levels = ps.int1("levels", ps.int1("nlevels", 3));
+            const Param* pi = ps.find("indices", {"integer"});
+            const Param* pp = ps.find("P", {"point"});
+            if (!pi) { warn("Vertex indices \"indices\" not provided for LoopSubdiv shape."); return; }
+            if (!pp) { warn("Vertex positions \"P\" not provided for LoopSubdiv shape."); return; }
+            std::vector<int> idx;
+            std::vector<float> P, sP, sN;
+            std::vector<int> sIdx;
+            for (double v : pi->nums) idx.push_back(int(v));
+            for (double v : pp->nums) P.push_back((float)v);
+            loop_subdivide(levels, idx, P, &sP, &sN, &sIdx);
+            add_mesh(ps, oflags, sP, sN, {}, {}, sIdx);
         } else if (name == "aaplane") {
             // CreateAAPlaneShape (plane.cpp:117-128)
             V3 lo = v3(0, 0, 0), hi = v3(0, 0, 0);

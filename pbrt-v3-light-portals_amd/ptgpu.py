@@ -146,6 +146,23 @@ class HostScene:
         d = ctypes.cast(ctypes.c_void_p(self.desc), ctypes.POINTER(_desc_prefix)).contents
         return [pt_material.from_buffer_copy(d.materials[i]) for i in range(d.n_materials)]
 
+    def mesh(self) -> dict:
+        """World-space vertex arrays and triangles of the flattened scene
+        (copies): P, N (None without shading normals), tri (m, 6) int32 =
+        v0 v1 v2 material area_light flags -- host only."""
+        d = ctypes.cast(ctypes.c_void_p(self.desc), ctypes.POINTER(_desc_prefix)).contents
+        nv, nt = d.n_vertices, d.n_triangles
+
+        def arr(ptr, n, dt):
+            if not ptr or n == 0:
+                return None
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(dt)), shape=(n,)).copy()
+        P = arr(d.P, 3 * nv, ctypes.c_float)
+        N = arr(d.N, 3 * nv, ctypes.c_float)
+        T = arr(d.triangles, 6 * nt, ctypes.c_int32)
+        return {"P": None if P is None else P.reshape(nv, 3), "N": None if N is None else N.reshape(nv, 3),
+                "tri": np.zeros((0, 6), np.int32) if T is None else T.reshape(nt, 6)}
+
     def film_size(self) -> Tuple[int, int]:
         """Cropped film (width, height) -- host only."""
         w, h = ctypes.c_int32(), ctypes.c_int32()

@@ -324,3 +324,16 @@ def test_multilobe_render_matches_oracle(tmp_path, material, strategy):
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst["closest_rays"] == rst["closest_rays"] and gst["shadow_rays"] == rst["shadow_rays"]
+
+
+def test_loopsubdiv_render_matches_oracle(tmp_path):
+    """A Loop-subdivided mesh (limit positions + shading normals, loopsubdiv.cpp)
+    under glossy plastic: device == oracle bit for bit."""
+    from test_loopsubdiv import _scene, icosa
+    P, idx = icosa()
+    hs, sc = _scene(_scene(tmp_path, P, idx, 2, xform="Rotate 20 0 1 0",
+                           material='Material "plastic" "rgb Kd" [0.4 0.2 0.2] "float roughness" [0.05]'))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst["closest_rays"] == rst["closest_rays"]
