@@ -329,9 +329,9 @@ def test_multilobe_render_matches_oracle(tmp_path, material, strategy):
 def test_loopsubdiv_render_matches_oracle(tmp_path):
     """A Loop-subdivided mesh (limit positions + shading normals, loopsubdiv.cpp)
     under glossy plastic: device == oracle bit for bit."""
-    from test_loopsubdiv import _scene, icosa
+    from test_loopsubdiv import _scene as loop_scene, icosa
     P, idx = icosa()
-    hs, sc = _scene(_scene(tmp_path, P, idx, 2, xform="Rotate 20 0 1 0",
+    hs, sc = _scene(loop_scene(tmp_path, P, idx, 2, xform="Rotate 20 0 1 0",
                            material='Material "plastic" "rgb Kd" [0.4 0.2 0.2] "float roughness" [0.05]'))
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     got, gst = sc.render()
