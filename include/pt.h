@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -54,7 +54,7 @@ typedef enum pt_status {
 
 /* ---- scene description (world space, the reference's post-parse Scene) ---- */
 
-enum pt_prim_kind { PT_PRIM_TRIANGLE = 0, PT_PRIM_AAPLANE = 1 };
+enum pt_prim_kind { PT_PRIM_TRIANGLE = 0, PT_PRIM_AAPLANE = 1, PT_PRIM_SPHERE = 2 };
 
 enum pt_material_kind {
     PT_MAT_NONE = 0,   /* "" / "none": null BSDF, path passes through   */
@@ -69,7 +69,8 @@ enum pt_material_kind {
 enum pt_light_kind {
     PT_LIGHT_DIFFUSE_AREA = 0, /* DiffuseAreaLight on one triangle   src/lights/diffuse.cpp */
     PT_LIGHT_PORTAL_AREA = 1,  /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
-    PT_LIGHT_INFINITE = 2      /* InfiniteAreaLight, constant L (no "mapname")  src/lights/infinite.cpp */
+    PT_LIGHT_INFINITE = 2,     /* InfiniteAreaLight, constant L (no "mapname")  src/lights/infinite.cpp */
+    PT_LIGHT_DIFFUSE_SPHERE = 3 /* DiffuseAreaLight on one sphere     src/lights/diffuse.cpp, shapes/sphere.cpp */
 };
 
 enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:12 */
@@ -115,10 +116,23 @@ typedef struct pt_aaplane {
     pt_transform object_to_world;  /* m = ObjectToWorld, minv = WorldToObject */
 } pt_aaplane;
 
+/* Sphere (src/shapes/sphere.{h,cpp}); parameters as given to
+ * CreateSphereShape (radius, zmin, zmax, phimax in degrees); the renderer
+ * derives the clamped Sphere members (sphere.h:50-59). */
+typedef struct pt_sphere {
+    float radius;
+    float zmin, zmax;
+    float phimax;
+    int32_t material;
+    int32_t area_light;
+    uint32_t flags;                /* PT_TRI_REVERSE_ORIENTATION | PT_TRI_SWAPS_HANDEDNESS */
+    pt_transform object_to_world;  /* m = ObjectToWorld, minv = WorldToObject */
+} pt_sphere;
+
 /* Primitive in scene order (RenderOptions::primitives, api.cpp:1431-1433). */
 typedef struct pt_prim {
     int32_t kind;   /* pt_prim_kind */
-    int32_t index;  /* into triangles or planes */
+    int32_t index;  /* into triangles, planes or spheres */
 } pt_prim;
 
 typedef struct pt_material {
@@ -151,7 +165,7 @@ typedef struct pt_light {
     int32_t kind;         /* pt_light_kind */
     float L[3];           /* Lemit = L * scale */
     int32_t two_sided;
-    int32_t shape;        /* triangle index (diffuse) or plane index (portal) */
+    int32_t shape;        /* triangle (diffuse), plane (portal) or sphere (diffuse sphere) index */
     int32_t strategy;     /* pt_portal_strategy (portal lights) */
     int32_t first_portal; /* into portals */
     int32_t n_portals;
@@ -216,6 +230,8 @@ typedef struct pt_scene_desc {
     pt_film_desc film;
     pt_sampler_desc sampler;
     pt_integrator_desc integrator;
+    int32_t n_spheres;
+    const pt_sphere* spheres;
 } pt_scene_desc;
 
 /* ---- statistics (reference counters, src/core/scene.cpp:40-42 etc.) ---- */

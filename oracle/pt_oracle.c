@@ -360,6 +360,14 @@ typedef struct {
     float area;                /* plane.h:29-31 */
 } Plane;
 
+/* Sphere (shapes/sphere.h:50-59): clamped members, transforms, center */
+typedef struct {
+    float radius, zMin, zMax, thetaMin, thetaMax, phiMax, area;
+    int ro, ro_xor_sh;
+    XF o2w, w2o;
+    V3 center; /* ObjectToWorld(Point3f(0, 0, 0)) */
+} Sphere;
+
 typedef struct {
     const pt_scene_desc* d;
     int nprims;
@@ -368,6 +376,7 @@ typedef struct {
     LNode* nodes;
     int nnodes;
     Plane* planes;
+    Sphere* spheres;
     float* tri_area;           /* per triangle (for triangle lights) */
     /* portal planes (AAPortal::portal), per desc portal */
     Plane* portal_planes;
@@ -808,7 +817,7 @@ static int plane_intersect(const Plane* pl, const Ray* ray, float* tHit, SI* si)
             V3 n = vnorm(vcross(dpdu, dpdv));
             V3 sn = n;
             if (pl->ro_xor_sh) { n = vmul(n, -1); sn = vmul(sn, -1); }
-            V3 wo = vnorm(vneg(ray->d));
+            V3 wo = vnorm(vneg(rT.d)); /* -ray.d of the object-space ray, normalised (Interaction ctor) */
             /* Transform::operator()(SurfaceInteraction) (transform.cpp:262-297) */
             const XF* t2 = &pl->o2w;
             si->p = xf_pt_err_in(&t2->m, pHit, err, &si->pError);
@@ -834,6 +843,200 @@ static void plane_sample(const Plane* pl, const float* u, V3* p, V3* n, V3* pErr
     *n = plane_normal(pl);
     *pErr = v3(0.1f, 0.1f, 0.1f);
     *pdf = 1 / pl->area;
+}
+
+/* ------------------------------------------------------------------------ */
+/* shapes/sphere.cpp with core/efloat.h running error bounds                 */
+/* ------------------------------------------------------------------------ */
+static float clampf11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); } /* Clamp (pbrt.h:309-316) */
+static float clampf_to(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static void sphere_init(Sphere* s, const pt_sphere* p) { /* Sphere ctor (sphere.h:50-59) */
+    float r = p->radius;
+    float zlo = fmins(p->zmin, p->zmax), zhi = fmaxs(p->zmin, p->zmax);
+    s->radius = r;
+    s->zMin = clampf_to(zlo, -r, r);
+    s->zMax = clampf_to(zhi, -r, r);
+    s->thetaMin = acosf(clampf_to(zlo / r, -1, 1));
+    s->thetaMax = acosf(clampf_to(zhi / r, -1, 1));
+    s->phiMax = (PI_F / 180) * clampf_to(p->phimax, 0, 360);
+    s->area = s->phiMax * s->radius * (s->zMax - s->zMin); /* Sphere::Area (sphere.cpp:224) */
+    s->ro = (p->flags & PT_TRI_REVERSE_ORIENTATION) != 0;
+    s->ro_xor_sh = s->ro ^ ((p->flags & PT_TRI_SWAPS_HANDEDNESS) != 0);
+    memcpy(s->o2w.m.m, p->object_to_world.m, 64);
+    memcpy(s->o2w.mi.m, p->object_to_world.minv, 64);
+    s->w2o.m = s->o2w.mi; s->w2o.mi = s->o2w.m;
+    s->center = xf_pt(&s->o2w.m, v3(0, 0, 0));
+}
+
+typedef struct { float v, lo, hi; } EFl; /* EFloat without the debug-only precise value */
+static EFl ef1(float v) { EFl r = {v, v, v}; return r; }
+static EFl ef_e(float v, float err) { /* EFloat(v, err) */
+    EFl r = {v, v, v};
+    if (err != 0.f) { r.lo = next_float_down(v - err); r.hi = next_float_up(v + err); }
+    return r;
+}
+static EFl ef_add(EFl a, EFl b) { EFl r = {a.v + b.v, next_float_down(a.lo + b.lo), next_float_up(a.hi + b.hi)}; return r; }
+static EFl ef_sub(EFl a, EFl b) { EFl r = {a.v - b.v, next_float_down(a.lo - b.hi), next_float_up(a.hi - b.lo)}; return r; }
+static EFl ef_mul(EFl a, EFl b) {
+    float p0 = a.lo * b.lo, p1 = a.hi * b.lo, p2 = a.lo * b.hi, p3 = a.hi * b.hi;
+    EFl r = {a.v * b.v, next_float_down(fmins(fmins(p0, p1), fmins(p2, p3))),
+             next_float_up(fmaxs(fmaxs(p0, p1), fmaxs(p2, p3)))};
+    return r;
+}
+static EFl ef_div(EFl a, EFl b) {
+    EFl r;
+    r.v = a.v / b.v;
+    if (b.lo < 0 && b.hi > 0) { r.lo = -INFINITY; r.hi = INFINITY; return r; }
+    float d0 = a.lo / b.lo, d1 = a.hi / b.lo, d2 = a.lo / b.hi, d3 = a.hi / b.hi;
+    r.lo = next_float_down(fmins(fmins(d0, d1), fmins(d2, d3)));
+    r.hi = next_float_up(fmaxs(fmaxs(d0, d1), fmaxs(d2, d3)));
+    return r;
+}
+static int ef_quadratic(EFl A, EFl B, EFl C, EFl* t0, EFl* t1) { /* efloat.h:266-287 */
+    double discrim = (double)B.v * (double)B.v - 4. * (double)A.v * (double)C.v;
+    if (discrim < 0.) return 0;
+    double rootDiscrim = sqrt(discrim);
+    EFl fr = ef_e((float)rootDiscrim, (float)((double)(FLT_EPSILON * 0.5f) * rootDiscrim));
+    EFl q = (B.v < 0) ? ef_mul(ef1(-.5f), ef_sub(B, fr)) : ef_mul(ef1(-.5f), ef_add(B, fr));
+    *t0 = ef_div(q, A);
+    *t1 = ef_div(C, q);
+    if (t0->v > t1->v) { EFl t = *t0; *t0 = *t1; *t1 = t; }
+    return 1;
+}
+/* Vector transform with absolute error (transform.h:337-352) */
+static V3 xf_vec_err(const M4* m, V3 v, V3* err) {
+    err->x = G3 * (fabsf(m->m[0][0] * v.x) + fabsf(m->m[0][1] * v.y) + fabsf(m->m[0][2] * v.z));
+    err->y = G3 * (fabsf(m->m[1][0] * v.x) + fabsf(m->m[1][1] * v.y) + fabsf(m->m[1][2] * v.z));
+    err->z = G3 * (fabsf(m->m[2][0] * v.x) + fabsf(m->m[2][1] * v.y) + fabsf(m->m[2][2] * v.z));
+    return xf_vec(m, v);
+}
+/* the clipped-sphere test on a candidate hit point (sphere.cpp:73-81) */
+static void sphere_point(const Sphere* s, V3 o, V3 d, float t, V3* pHit, float* phi) {
+    V3 p = vadd(o, vmul(d, t));
+    p = vmul(p, s->radius / vlen(p));
+    if (p.x == 0 && p.y == 0) p.x = 1e-5f * s->radius;
+    float ph = atan2f(p.y, p.x);
+    if (ph < 0) ph += 2 * PI_F;
+    *pHit = p; *phi = ph;
+}
+static int sphere_clipped(const Sphere* s, V3 p, float phi) {
+    return (s->zMin > -s->radius && p.z < s->zMin) || (s->zMax < s->radius && p.z > s->zMax) || phi > s->phiMax;
+}
+/* Sphere::Intersect (sphere.cpp:50-146); IntersectP (148-200) is the same
+ * test without the SurfaceInteraction (si == NULL). */
+static int sphere_intersect(const Sphere* s, const Ray* r, float* tHit, SI* si) {
+    V3 oErr, dErr;
+    V3 o = xf_pt_err(&s->w2o.m, r->o, &oErr);
+    V3 d = xf_vec_err(&s->w2o.m, r->d, &dErr);
+    float l2 = vlen2(d);
+    if (l2 > 0) { /* Transform::operator()(Ray, oError*, dError*) (transform.h:382-394) */
+        float dt = vdot(vabs(d), oErr) / l2;
+        o = vadd(o, vmul(d, dt));
+    }
+    EFl ox = ef_e(o.x, oErr.x), oy = ef_e(o.y, oErr.y), oz = ef_e(o.z, oErr.z);
+    EFl dx = ef_e(d.x, dErr.x), dy = ef_e(d.y, dErr.y), dz = ef_e(d.z, dErr.z);
+    EFl a = ef_add(ef_add(ef_mul(dx, dx), ef_mul(dy, dy)), ef_mul(dz, dz));
+    EFl b = ef_mul(ef1(2.f), ef_add(ef_add(ef_mul(dx, ox), ef_mul(dy, oy)), ef_mul(dz, oz)));
+    EFl c = ef_sub(ef_add(ef_add(ef_mul(ox, ox), ef_mul(oy, oy)), ef_mul(oz, oz)),
+                   ef_mul(ef1(s->radius), ef1(s->radius)));
+    EFl t0, t1;
+    if (!ef_quadratic(a, b, c, &t0, &t1)) return 0;
+    if (t0.hi > r->tMax || t1.lo <= 0) return 0;
+    EFl ts = t0;
+    if (ts.lo <= 0) {
+        ts = t1;
+        if (ts.hi > r->tMax) return 0;
+    }
+    V3 pHit;
+    float phi;
+    sphere_point(s, o, d, ts.v, &pHit, &phi);
+    if (sphere_clipped(s, pHit, phi)) {
+        if (ts.v == t1.v) return 0; /* EFloat::operator== compares v */
+        if (t1.hi > r->tMax) return 0;
+        ts = t1;
+        sphere_point(s, o, d, ts.v, &pHit, &phi);
+        if (sphere_clipped(s, pHit, phi)) return 0;
+    }
+    if (tHit) *tHit = ts.v;
+    if (si) {
+        float theta = acosf(clampf11(pHit.z / s->radius));
+        float zRadius = sqrtf(pHit.x * pHit.x + pHit.y * pHit.y);
+        float invZRadius = 1 / zRadius;
+        float cosPhi = pHit.x * invZRadius, sinPhi = pHit.y * invZRadius;
+        V3 dpdu = v3(-s->phiMax * pHit.y, s->phiMax * pHit.x, 0);
+        V3 dpdv = fmulv(s->thetaMax - s->thetaMin, v3(pHit.z * cosPhi, pHit.z * sinPhi, -s->radius * sinf(theta)));
+        V3 pError = fmulv(G5, vabs(pHit));
+        /* SurfaceInteraction ctor (interaction.cpp:44-70) */
+        V3 n = vnorm(vcross(dpdu, dpdv));
+        if (s->ro_xor_sh) n = vmul(n, -1);
+        V3 wo = vnorm(vneg(d));
+        /* Transform::operator()(SurfaceInteraction) (transform.cpp:262-297) */
+        si->p = xf_pt_err_in(&s->o2w.m, pHit, pError, &si->pError);
+        si->n = vnorm(xf_nrm(&s->o2w, n));
+        si->wo = vnorm(xf_vec(&s->o2w.m, wo));
+        si->dpdu = xf_vec(&s->o2w.m, dpdu);
+        si->sn = vnorm(xf_nrm(&s->o2w, n));
+        si->sdpdu = xf_vec(&s->o2w.m, dpdu);
+        si->sn = faceforward(si->sn, si->n);
+    }
+    return 1;
+}
+/* Sphere::Sample(u, pdf) (sphere.cpp:226-236) */
+static void sphere_sample_area(const Sphere* s, const float* u, V3* p, V3* n, V3* pErr, float* pdf) {
+    float z = 1 - 2 * u[0]; /* UniformSampleSphere (sampling.cpp:98-103) */
+    float r = sqrtf(fmaxs(0.f, 1.f - z * z));
+    float phi = 2 * PI_F * u[1];
+    V3 w = v3(r * cosf(phi), r * sinf(phi), z);
+    V3 pObj = vadd(v3(0, 0, 0), vmul(w, s->radius));
+    *n = vnorm(xf_nrm(&s->o2w, pObj));
+    if (s->ro) *n = vmul(*n, -1);
+    pObj = vmul(pObj, s->radius / vlen(pObj));
+    V3 pObjError = fmulv(G5, vabs(pObj));
+    *p = xf_pt_err_in(&s->o2w.m, pObj, pObjError, pErr);
+    *pdf = 1 / s->area;
+}
+/* Sphere::Sample(ref, u, pdf) (sphere.cpp:238-301) */
+static void sphere_sample_ref(const Sphere* s, const SI* ref, const float* u, V3* p, V3* n, V3* pErr, float* pdf) {
+    V3 pCenter = s->center;
+    V3 pOrigin = offset_ray_origin(ref->p, ref->pError, ref->n, vsub(pCenter, ref->p));
+    if (dist2(pOrigin, pCenter) <= s->radius * s->radius) {
+        sphere_sample_area(s, u, p, n, pErr, pdf);
+        V3 wi = vsub(*p, ref->p);
+        if (vlen2(wi) == 0) *pdf = 0;
+        else {
+            wi = vnorm(wi);
+            *pdf *= dist2(ref->p, *p) / vabsdot(*n, vneg(wi));
+        }
+        if (isinf(*pdf)) *pdf = 0.f;
+        return;
+    }
+    float dc = vlen(vsub(ref->p, pCenter));
+    float invDc = 1 / dc;
+    V3 wc = vmul(vsub(pCenter, ref->p), invDc);
+    V3 wcX, wcY;
+    coordinate_system(wc, &wcX, &wcY);
+    float sinThetaMax = s->radius * invDc;
+    float sinThetaMax2 = sinThetaMax * sinThetaMax;
+    float invSinThetaMax = 1 / sinThetaMax;
+    float cosThetaMax = sqrtf(fmaxs(0.f, 1 - sinThetaMax2));
+    float cosTheta = (cosThetaMax - 1) * u[0] + 1;
+    float sinTheta2 = 1 - cosTheta * cosTheta;
+    if (sinThetaMax2 < 0.00068523f) { /* sin^2(1.5 deg) */
+        sinTheta2 = sinThetaMax2 * u[0];
+        cosTheta = sqrtf(1 - sinTheta2);
+    }
+    float cosAlpha = sinTheta2 * invSinThetaMax +
+                     cosTheta * sqrtf(fmaxs(0.f, 1.f - sinTheta2 * invSinThetaMax * invSinThetaMax));
+    float sinAlpha = sqrtf(fmaxs(0.f, 1.f - cosAlpha * cosAlpha));
+    float phi = u[1] * 2 * PI_F;
+    /* SphericalDirection(sinAlpha, cosAlpha, phi, -wcX, -wcY, -wc) (geometry.h:1629-1634) */
+    V3 nW = vadd(vadd(vmul(vneg(wcX), sinAlpha * cosf(phi)), vmul(vneg(wcY), sinAlpha * sinf(phi))),
+                 vmul(vneg(wc), cosAlpha));
+    V3 pW = vadd(pCenter, vmul(nW, s->radius));
+    *p = pW;
+    *pErr = fmulv(G5, vabs(pW));
+    *n = s->ro ? vmul(nW, -1) : nW;
+    *pdf = 1 / (2 * PI_F * (1 - cosThetaMax));
 }
 
 /* ------------------------------------------------------------------------ */
@@ -957,10 +1160,18 @@ static BB prim_world_bound(const Scene* sc, int kind, int idx) {
         const pt_triangle* t = &d->triangles[idx];
         return bb_unionp(bb_pp(vtx(d, t->v[0]), vtx(d, t->v[1])), vtx(d, t->v[2]));
     }
-    /* Shape::WorldBound = ObjectToWorld(ObjectBound{lo,hi}) (shape.cpp:52, transform.cpp:230-241) */
-    const Plane* pl = &sc->planes[idx];
-    BB b = bb_pp(pl->lo, pl->hi);
-    const M4* m = &pl->o2w.m;
+    /* Shape::WorldBound = ObjectToWorld(ObjectBound()) (shape.cpp:52, transform.cpp:238-249) */
+    BB b;
+    const M4* m;
+    if (kind == PT_PRIM_SPHERE) { /* Sphere::ObjectBound (sphere.cpp:44-47) */
+        const Sphere* sp = &sc->spheres[idx];
+        b = bb_pp(v3(-sp->radius, -sp->radius, sp->zMin), v3(sp->radius, sp->radius, sp->zMax));
+        m = &sp->o2w.m;
+    } else {
+        const Plane* pl = &sc->planes[idx];
+        b = bb_pp(pl->lo, pl->hi);
+        m = &pl->o2w.m;
+    }
     V3 mn = b.pmin, mx = b.pmax;
     BB r; V3 q = xf_pt(m, v3(mn.x, mn.y, mn.z)); r.pmin = q; r.pmax = q;
     r = bb_unionp(r, xf_pt(m, v3(mx.x, mn.y, mn.z)));
@@ -1050,6 +1261,8 @@ static int scene_intersect(const Scene* sc, Ray* ray, SI* si, Counters* ctr) {
                     ctr->prims++;
                     if (sc->prim_kind[pi] == PT_PRIM_TRIANGLE)
                         ok = tri_intersect(sc->d, sc->prim_index[pi], ray, &t, NULL, 1);
+                    else if (sc->prim_kind[pi] == PT_PRIM_SPHERE)
+                        ok = sphere_intersect(&sc->spheres[sc->prim_index[pi]], ray, &t, NULL);
                     else
                         ok = plane_intersect(&sc->planes[sc->prim_index[pi]], ray, &t, NULL);
                     if (ok) { ray->tMax = t; hit = 1; hitPrim = pi; } /* GeometricPrimitive::Intersect */
@@ -1070,6 +1283,8 @@ static int scene_intersect(const Scene* sc, Ray* ray, SI* si, Counters* ctr) {
         Ray r2 = *ray; r2.tMax = INFINITY;
         float t;
         if (sc->prim_kind[hitPrim] == PT_PRIM_TRIANGLE) tri_intersect(sc->d, sc->prim_index[hitPrim], &r2, &t, si, 1);
+        else if (sc->prim_kind[hitPrim] == PT_PRIM_SPHERE)
+            sphere_intersect(&sc->spheres[sc->prim_index[hitPrim]], &r2, &t, si);
         else plane_intersect(&sc->planes[sc->prim_index[hitPrim]], &r2, &t, si);
         si->prim = hitPrim;
     }
@@ -1097,6 +1312,8 @@ static int scene_intersect_p(const Scene* sc, const Ray* ray, Counters* ctr) {
                      * Intersect (shape.h:58-62) */
                     if (sc->prim_kind[pi] == PT_PRIM_TRIANGLE)
                         ok = tri_intersect(sc->d, sc->prim_index[pi], ray, NULL, NULL, 0);
+                    else if (sc->prim_kind[pi] == PT_PRIM_SPHERE)
+                        ok = sphere_intersect(&sc->spheres[sc->prim_index[pi]], ray, NULL, NULL);
                     else
                         ok = plane_intersect(&sc->planes[sc->prim_index[pi]], ray, NULL, NULL);
                     if (ok) return 1;
@@ -1119,7 +1336,6 @@ static int scene_intersect_p(const Scene* sc, const Ray* ray, Counters* ctr) {
 /* Microfacet distribution and Fresnel (core/microfacet.{h,cpp},             */
 /* core/reflection.{h,cpp})                                                  */
 /* ------------------------------------------------------------------------ */
-static float clampf11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); } /* Clamp (pbrt.h:309-316) */
 static float cos2t(V3 w) { return w.z * w.z; }                               /* reflection.h:57-90 */
 static float sin2t(V3 w) { return fmaxs((float)0, (float)1 - cos2t(w)); }
 static float sint(V3 w) { return sqrtf(sin2t(w)); }
@@ -1552,19 +1768,22 @@ static RGB area_L(const pt_light* l, V3 n, V3 w) { /* diffuse.h:58-60 */
     return (l->two_sided || vdot(n, w) > 0) ? rgbv(l->L) : rgb1(0);
 }
 /* SurfaceInteraction::Le (interaction.cpp:148-151) */
-static RGB si_Le(const Scene* sc, const SI* si, V3 w) {
+static int si_light(const Scene* sc, const SI* si) {
     int kind = sc->prim_kind[si->prim], idx = sc->prim_index[si->prim];
-    int li = kind == PT_PRIM_TRIANGLE ? sc->d->triangles[idx].area_light : sc->d->planes[idx].area_light;
+    if (kind == PT_PRIM_TRIANGLE) return sc->d->triangles[idx].area_light;
+    if (kind == PT_PRIM_SPHERE) return sc->d->spheres[idx].area_light;
+    return sc->d->planes[idx].area_light;
+}
+static RGB si_Le(const Scene* sc, const SI* si, V3 w) {
+    int li = si_light(sc, si);
     if (li < 0) return rgb1(0);
     return area_L(&sc->d->lights[li], si->n, w);
 }
-static int si_light(const Scene* sc, const SI* si) {
-    int kind = sc->prim_kind[si->prim], idx = sc->prim_index[si->prim];
-    return kind == PT_PRIM_TRIANGLE ? sc->d->triangles[idx].area_light : sc->d->planes[idx].area_light;
-}
 static int si_material(const Scene* sc, const SI* si) {
     int kind = sc->prim_kind[si->prim], idx = sc->prim_index[si->prim];
-    return kind == PT_PRIM_TRIANGLE ? sc->d->triangles[idx].material : sc->d->planes[idx].material;
+    if (kind == PT_PRIM_TRIANGLE) return sc->d->triangles[idx].material;
+    if (kind == PT_PRIM_SPHERE) return sc->d->spheres[idx].material;
+    return sc->d->planes[idx].material;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1694,6 +1913,13 @@ static RGB area_sample_li(const Scene* sc, const pt_light* l, const SI* ref, con
         *spErr = v3(0, 0, 0);
         return inf_sample_li(&sc->inf[l - sc->d->lights], ref, u, wi, pdf, sp);
     }
+    if (l->kind == PT_LIGHT_DIFFUSE_SPHERE) { /* Sphere::Sample(ref, u, pdf) override */
+        sphere_sample_ref(&sc->spheres[l->shape], ref, u, &p, &n, &pe, pdf);
+        if (*pdf == 0 || vlen2(vsub(p, ref->p)) == 0) { *pdf = 0; return rgb1(0); }
+        *wi = vnorm(vsub(p, ref->p));
+        *sp = p; *sn = n; *spErr = pe;
+        return area_L(l, n, vneg(*wi));
+    }
     if (l->kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l->shape, u, &p, &n, &pe, pdf);
     else plane_sample(&sc->planes[l->shape], u, &p, &n, &pe, pdf);
     V3 w = vsub(p, ref->p);
@@ -1717,7 +1943,17 @@ static float area_pdf_li(const Scene* sc, const pt_light* l, const SI* ref, V3 w
     float tHit;
     int ok;
     float area;
-    if (l->kind == PT_LIGHT_DIFFUSE_AREA) {
+    if (l->kind == PT_LIGHT_DIFFUSE_SPHERE) { /* Sphere::Pdf (sphere.cpp:303-315) */
+        const Sphere* s = &sc->spheres[l->shape];
+        V3 pOrigin = offset_ray_origin(ref->p, ref->pError, ref->n, vsub(s->center, ref->p));
+        if (!(dist2(pOrigin, s->center) <= s->radius * s->radius)) {
+            float sinThetaMax2 = s->radius * s->radius / dist2(ref->p, s->center);
+            float cosThetaMax = sqrtf(fmaxs(0, 1 - sinThetaMax2));
+            return 1 / (2 * PI_F * (1 - cosThetaMax)); /* UniformConePdf (sampling.cpp:132-134) */
+        }
+        ok = sphere_intersect(s, &r, &tHit, &isl);
+        area = s->area;
+    } else if (l->kind == PT_LIGHT_DIFFUSE_AREA) {
         ok = tri_intersect(sc->d, l->shape, &r, &tHit, &isl, 1);
         area = sc->tri_area[l->shape];
     } else {
@@ -2122,6 +2358,8 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     ensure_init();
     memset(sc, 0, sizeof *sc);
     sc->d = d;
+    sc->spheres = (Sphere*)calloc((size_t)(d->n_spheres + 1), sizeof(Sphere));
+    for (int i = 0; i < d->n_spheres; ++i) sphere_init(&sc->spheres[i], &d->spheres[i]);
     sc->planes = (Plane*)calloc((size_t)(d->n_planes + 1), sizeof(Plane));
     for (int i = 0; i < d->n_planes; ++i) {
         const pt_aaplane* p = &d->planes[i];
@@ -2161,7 +2399,9 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
                 sc->ldist_func[i] = sy(smulf(lmap_lookup(I, .5f, .5f), PI_F * I->radius * I->radius));
                 continue;
             }
-            float area = l->kind == PT_LIGHT_DIFFUSE_AREA ? sc->tri_area[l->shape] : sc->planes[l->shape].area;
+            float area = l->kind == PT_LIGHT_DIFFUSE_AREA     ? sc->tri_area[l->shape]
+                         : l->kind == PT_LIGHT_DIFFUSE_SPHERE ? sc->spheres[l->shape].area
+                                                               : sc->planes[l->shape].area;
             /* DiffuseAreaLight::Power() = (twoSided ? 2 : 1) * Lemit * area * Pi (diffuse.cpp:62-64) */
             RGB pw = smulf(smulf(smulf(rgbv(l->L), (float)(l->two_sided ? 2 : 1)), area), PI_F);
             sc->ldist_func[i] = sy(pw);
@@ -2189,7 +2429,7 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     return 0;
 }
 static void scene_free(Scene* sc) {
-    free(sc->planes); free(sc->tri_area); free(sc->portal_planes);
+    free(sc->planes); free(sc->spheres); free(sc->tri_area); free(sc->portal_planes);
     free(sc->prim_kind); free(sc->prim_index); free(sc->nodes);
     free(sc->ldist_func); free(sc->ldist_cdf); free(sc->inf);
 }

@@ -174,11 +174,19 @@ BBox prim_world_bound(const pt_scene_desc* d, int i) {
         auto P = [&](int k) { return v3(d->P[3 * k], d->P[3 * k + 1], d->P[3 * k + 2]); };
         return bb_union(bb_points(P(t.v[0]), P(t.v[1])), P(t.v[2]));
     }
-    // Shape::WorldBound = ObjectToWorld(ObjectBound{lo, hi}) (transform.cpp:230-241)
-    const pt_aaplane& pl = d->planes[p.index];
-    BBox ob = bb_points(v3(pl.lo[0], pl.lo[1], pl.lo[2]), v3(pl.hi[0], pl.hi[1], pl.hi[2]));
+    // Shape::WorldBound = ObjectToWorld(ObjectBound()) (shape.cpp:52, transform.cpp:238-249)
+    BBox ob;
     M4 m;
-    std::memcpy(m.m, pl.object_to_world.m, 64);
+    if (p.kind == PT_PRIM_SPHERE) {  // Sphere::ObjectBound (sphere.cpp:44-47)
+        const pt_sphere& sp = d->spheres[p.index];
+        const SphereMembers sm = sphere_members(sp);
+        ob = bb_points(v3(-sm.radius, -sm.radius, sm.zmin), v3(sm.radius, sm.radius, sm.zmax));
+        std::memcpy(m.m, sp.object_to_world.m, 64);
+    } else {
+        const pt_aaplane& pl = d->planes[p.index];
+        ob = bb_points(v3(pl.lo[0], pl.lo[1], pl.lo[2]), v3(pl.hi[0], pl.hi[1], pl.hi[2]));
+        std::memcpy(m.m, pl.object_to_world.m, 64);
+    }
     V3 a = ob.pmin, b = ob.pmax;
     V3 q = xf_point(m, v3(a.x, a.y, a.z));
     BBox r{q, q};

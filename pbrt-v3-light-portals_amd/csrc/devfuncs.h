@@ -286,7 +286,7 @@ __device__ __forceinline__ bool plane_surface(const DevPlane& pl, const Ray& ray
     V3 n = normalize(cross(dpdu, dpdv));
     V3 sn = n;
     if (pl.ro_xor_sh) { n = n * -1.f; sn = sn * -1.f; }
-    V3 wo = normalize(-ray.d);
+    V3 wo = normalize(-xf_vector(pl.w2o, ray.d));  // -ray.d of the object-space ray, normalised (Interaction ctor)
     si->p = xf_point_err_in(pl.o2w, pHit, v3(0.01f, 0.01f, 0.01f), &si->perr);
     si->n = normalize(xf_normal(pl.w2o, n));
     si->wo = normalize(xf_vector(pl.o2w, wo));
@@ -296,22 +296,149 @@ __device__ __forceinline__ bool plane_surface(const DevPlane& pl, const Ray& ray
     return true;
 }
 
+// ----------------------------------------------------------------------------
+// Sphere (shapes/sphere.cpp) with EFloat running error bounds (core/efloat.h)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float clamp11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); }
+struct EF {
+    float v, lo, hi;
+};
+__device__ __forceinline__ EF ef(float v) { return EF{v, v, v}; }
+__device__ __forceinline__ EF ef_err(float v, float err) {  // EFloat(v, err)
+    if (err == 0.f) return EF{v, v, v};
+    return EF{v, next_down(v - err), next_up(v + err)};
+}
+__device__ __forceinline__ EF operator+(EF a, EF b) { return EF{a.v + b.v, next_down(a.lo + b.lo), next_up(a.hi + b.hi)}; }
+__device__ __forceinline__ EF operator-(EF a, EF b) { return EF{a.v - b.v, next_down(a.lo - b.hi), next_up(a.hi - b.lo)}; }
+__device__ __forceinline__ EF operator*(EF a, EF b) {
+    const float p0 = a.lo * b.lo, p1 = a.hi * b.lo, p2 = a.lo * b.hi, p3 = a.hi * b.hi;
+    return EF{a.v * b.v, next_down(smin(smin(p0, p1), smin(p2, p3))), next_up(smax(smax(p0, p1), smax(p2, p3)))};
+}
+__device__ __forceinline__ EF operator/(EF a, EF b) {
+    if (b.lo < 0 && b.hi > 0) return EF{a.v / b.v, -kInf, kInf};
+    const float d0 = a.lo / b.lo, d1 = a.hi / b.lo, d2 = a.lo / b.hi, d3 = a.hi / b.hi;
+    return EF{a.v / b.v, next_down(smin(smin(d0, d1), smin(d2, d3))), next_up(smax(smax(d0, d1), smax(d2, d3)))};
+}
+// Quadratic(EFloat...) (efloat.h:266-287)
+__device__ __forceinline__ bool ef_quadratic(EF A, EF B, EF C, EF* t0, EF* t1) {
+    const double discrim = (double)B.v * (double)B.v - 4. * (double)A.v * (double)C.v;
+    if (discrim < 0.) return false;
+    const double rootDiscrim = sqrt(discrim);
+    const EF fr = ef_err((float)rootDiscrim, (float)((double)(kMachineEps) * rootDiscrim));
+    const EF q = (B.v < 0) ? ef(-.5f) * (B - fr) : ef(-.5f) * (B + fr);
+    *t0 = q / A;
+    *t1 = C / q;
+    if (t0->v > t1->v) { const EF t = *t0; *t0 = *t1; *t1 = t; }
+    return true;
+}
+
+// Sphere::Intersect / IntersectP up to the accepted hit (sphere.cpp:50-112 /
+// 148-200): object-space ray with error bounds, conservative roots, partial
+// sphere clipping with the second root.  Returns the hit distance, the
+// object-space point and phi.
+__device__ __forceinline__ bool sphere_test(const DevSphere& s, const Ray& r, float* tHit, V3* pHitOut) {
+    V3 oErr, dErr;
+    V3 o = xf_point_err(s.w2o, r.o, &oErr);
+    const V3 d = xf_vector_err(s.w2o, r.d, &dErr);
+    const float l2 = len2(d);
+    if (l2 > 0) {  // Transform::operator()(Ray, oError, dError) (transform.h:382-394)
+        const float dt = dot(vabs(d), oErr) / l2;
+        o = o + d * dt;
+    }
+    const EF ox = ef_err(o.x, oErr.x), oy = ef_err(o.y, oErr.y), oz = ef_err(o.z, oErr.z);
+    const EF dx = ef_err(d.x, dErr.x), dy = ef_err(d.y, dErr.y), dz = ef_err(d.z, dErr.z);
+    const EF a = dx * dx + dy * dy + dz * dz;
+    const EF b = ef(2.f) * (dx * ox + dy * oy + dz * oz);
+    const EF c = ox * ox + oy * oy + oz * oz - ef(s.radius) * ef(s.radius);
+    EF t0, t1;
+    if (!ef_quadratic(a, b, c, &t0, &t1)) return false;
+    if (t0.hi > r.tmax || t1.lo <= 0) return false;
+    EF ts = t0;
+    if (ts.lo <= 0) {
+        ts = t1;
+        if (ts.hi > r.tmax) return false;
+    }
+    const float twoPi = 2 * kPi;
+    V3 pHit = o + d * ts.v;
+    pHit = pHit * (s.radius / len(pHit));
+    if (pHit.x == 0 && pHit.y == 0) pHit.x = 1e-5f * s.radius;
+    float phi = libm_atan2f(pHit.y, pHit.x);
+    if (phi < 0) phi += twoPi;
+    if ((s.zmin > -s.radius && pHit.z < s.zmin) || (s.zmax < s.radius && pHit.z > s.zmax) || phi > s.phi_max) {
+        if (ts.v == t1.v) return false;
+        if (t1.hi > r.tmax) return false;
+        ts = t1;
+        pHit = o + d * ts.v;
+        pHit = pHit * (s.radius / len(pHit));
+        if (pHit.x == 0 && pHit.y == 0) pHit.x = 1e-5f * s.radius;
+        phi = libm_atan2f(pHit.y, pHit.x);
+        if (phi < 0) phi += twoPi;
+        if ((s.zmin > -s.radius && pHit.z < s.zmin) || (s.zmax < s.radius && pHit.z > s.zmax) || phi > s.phi_max)
+            return false;
+    }
+    *tHit = ts.v;
+    *pHitOut = pHit;
+    return true;
+}
+
+// SurfaceInteraction of Sphere::Intersect (sphere.cpp:114-140), to world space
+// (transform.cpp:262-297).  Only what shading reads: p, pError, n, shading
+// n and dpdu.
+__device__ __forceinline__ bool sphere_surface(const DevSphere& s, const Ray& ray, SurfHit* si) {
+    Ray r2 = ray;
+    r2.tmax = kInf;
+    float t;
+    V3 pHit;
+    if (!sphere_test(s, r2, &t, &pHit)) return false;
+    const float theta = libm_acosf(clamp11(pHit.z / s.radius));
+    const float zRadius = sqrtf(pHit.x * pHit.x + pHit.y * pHit.y);
+    const float invZRadius = 1 / zRadius;
+    const float cosPhi = pHit.x * invZRadius, sinPhi = pHit.y * invZRadius;
+    const V3 dpdu = v3(-s.phi_max * pHit.y, s.phi_max * pHit.x, 0);
+    const V3 dpdv = (s.theta_max - s.theta_min) * v3(pHit.z * cosPhi, pHit.z * sinPhi, -s.radius * libm_sinf(theta));
+    V3 n = normalize(cross(dpdu, dpdv));
+    if (s.ro_xor_sh) n = n * -1.f;
+    const V3 pError = gammaf(5) * vabs(pHit);
+    si->p = xf_point_err_in(s.o2w, pHit, pError, &si->perr);
+    si->n = normalize(xf_normal(s.w2o, n));
+    si->wo = normalize(xf_vector(s.o2w, normalize(-xf_vector(s.w2o, ray.d))));  // Interaction ctor normalises wo
+    si->sn = faceforward(si->n, si->n);
+    si->sdpdu = xf_vector(s.o2w, dpdu);
+    return true;
+}
+
+// Leaf test of a non-triangle primitive record (plane, or sphere when the
+// kernel is compiled with kSph).
+template <bool kSph = true>
+__device__ __forceinline__ bool shape_test(const DevScene& sc, uint32_t flags, int idx, const Ray& ray, float* t) {
+    V3 ph;
+    if (kSph && (flags & kPrimSphere)) return sphere_test(sc.spheres[idx], ray, t, &ph);
+    return plane_test(sc.planes[idx], ray, t, &ph);
+}
+
+template <bool kSph = true>
 __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
     float4 r0 = sc.prims[3 * prim];
     float4 r1 = sc.prims[3 * prim + 1];
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
-    bool ok = (flags & kPrimPlane) ? plane_surface(sc.planes[idx], ray, si) : tri_surface(sc, idx, ray, si);
+    bool ok = (kSph && (flags & kPrimSphere)) ? sphere_surface(sc.spheres[idx], ray, si)
+              : (flags & kPrimPlane) ? plane_surface(sc.planes[idx], ray, si)
+                                     : tri_surface(sc, idx, ray, si);
     si->prim = prim;
     return ok;
 }
 
+template <bool kSph = true>
 __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
     float4 r0 = sc.prims[3 * prim];
     float4 r1 = sc.prims[3 * prim + 1];
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
-    if (flags & kPrimPlane) {
+    if (kSph && (flags & kPrimSphere)) {
+        *material = sc.spheres[idx].material;
+        *light = sc.spheres[idx].area_light;
+    } else if (flags & kPrimPlane) {
         *material = sc.planes[idx].material;
         *light = sc.planes[idx].area_light;
     } else {
@@ -329,7 +456,6 @@ __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* mat
 // Shading-frame trigonometry (reflection.h:55-90) and the Trowbridge-Reitz
 // microfacet distribution (microfacet.h:105-133, microfacet.cpp:155-345)
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ float clamp11(float v) { return v < -1 ? -1.f : (v > 1 ? 1.f : v); }
 __device__ __forceinline__ float cos2_theta(V3 w) { return w.z * w.z; }
 __device__ __forceinline__ float sin2_theta(V3 w) { return smax(0.f, 1.f - cos2_theta(w)); }
 __device__ __forceinline__ float sin_theta(V3 w) { return sqrtf(sin2_theta(w)); }
@@ -450,13 +576,15 @@ enum : int {
     kFtMicro = 1,       // metal, plastic, rough glass: microfacet lobes, two-lobe BSDFs
     kFtSpecular = 2,    // smooth glass, dispersive glass, mirror: specular lobes
     kFtInfinite = 4,    // an InfiniteAreaLight
-    kFtAll = 7
+    kFtSphere = 8,      // Sphere shapes (and sphere area lights)
+    kFtAll = 15
 };
 template <int kFt>
 struct Ft {
     static constexpr bool micro = (kFt & kFtMicro) != 0;
     static constexpr bool spec = (kFt & kFtSpecular) != 0;
     static constexpr bool inf = (kFt & kFtInfinite) != 0;
+    static constexpr bool sph = (kFt & kFtSphere) != 0;
     static constexpr int max_lobes = micro ? 2 : 1;
 };
 
@@ -881,6 +1009,68 @@ __device__ __forceinline__ float inf_pdf_li(const DevLight& l, V3 w) {
     return (l.cfunc[2 * iv + iu] / l.mint) / (2 * kPi * kPi * sinTheta);
 }
 
+// Sphere::Sample(u, pdf) (sphere.cpp:226-236): uniform area sample
+__device__ __forceinline__ void sphere_sample_area(const DevSphere& s, float u0, float u1, V3* p, V3* n, V3* perr,
+                                                   float* pdf) {
+    // UniformSampleSphere (sampling.cpp:98-103)
+    const float z = 1 - 2 * u0;
+    const float r = sqrtf(smax(0.f, 1.f - z * z));
+    const float phi = 2 * kPi * u1;
+    const V3 w = v3(r * libm_cosf(phi), r * libm_sinf(phi), z);
+    V3 pObj = v3(0, 0, 0) + w * s.radius;
+    *n = normalize(xf_normal(s.w2o, pObj));
+    if (s.ro) *n = *n * -1.f;
+    pObj = pObj * (s.radius / len(pObj));
+    const V3 pObjError = gammaf(5) * vabs(pObj);
+    *p = xf_point_err_in(s.o2w, pObj, pObjError, perr);
+    *pdf = 1 / s.area;
+}
+
+// Sphere::Sample(ref, u, pdf) (sphere.cpp:238-301): area sampling from inside,
+// else uniform sampling of the subtended cone (with the small-angle branch).
+__device__ __forceinline__ void sphere_sample_ref(const DevSphere& s, const SurfHit& ref, float u0, float u1, V3* p,
+                                                  V3* n, V3* perr, float* pdf) {
+    const V3 pCenter = s.center;
+    const V3 pOrigin = offset_ray_origin(ref.p, ref.perr, ref.n, pCenter - ref.p);
+    if (dist2(pOrigin, pCenter) <= s.radius * s.radius) {
+        sphere_sample_area(s, u0, u1, p, n, perr, pdf);
+        V3 wi = *p - ref.p;
+        if (len2(wi) == 0) *pdf = 0;
+        else {
+            wi = normalize(wi);
+            *pdf *= dist2(ref.p, *p) / absdot(*n, -wi);
+        }
+        if (__builtin_isinf(*pdf)) *pdf = 0.f;
+        return;
+    }
+    const float dc = len(ref.p - pCenter);
+    const float invDc = 1 / dc;
+    const V3 wc = (pCenter - ref.p) * invDc;
+    V3 wcX, wcY;
+    coordinate_system(wc, &wcX, &wcY);
+    const float sinThetaMax = s.radius * invDc;
+    const float sinThetaMax2 = sinThetaMax * sinThetaMax;
+    const float invSinThetaMax = 1 / sinThetaMax;
+    const float cosThetaMax = sqrtf(smax(0.f, 1 - sinThetaMax2));
+    float cosTheta = (cosThetaMax - 1) * u0 + 1;
+    float sinTheta2 = 1 - cosTheta * cosTheta;
+    if (sinThetaMax2 < 0.00068523f) {  // sin^2(1.5 deg): Taylor expansion branch
+        sinTheta2 = sinThetaMax2 * u0;
+        cosTheta = sqrtf(1 - sinTheta2);
+    }
+    const float cosAlpha = sinTheta2 * invSinThetaMax +
+                           cosTheta * sqrtf(smax(0.f, 1.f - sinTheta2 * invSinThetaMax * invSinThetaMax));
+    const float sinAlpha = sqrtf(smax(0.f, 1.f - cosAlpha * cosAlpha));
+    const float phi = u1 * 2 * kPi;
+    // SphericalDirection(sinAlpha, cosAlpha, phi, -wcX, -wcY, -wc) (geometry.h:1629-1634)
+    const V3 nWorld = ((-wcX) * (sinAlpha * libm_cosf(phi)) + (-wcY) * (sinAlpha * libm_sinf(phi))) + (-wc) * cosAlpha;
+    const V3 pWorld = pCenter + nWorld * s.radius;
+    *p = pWorld;
+    *perr = gammaf(5) * vabs(pWorld);
+    *n = s.ro ? nWorld * -1.f : nWorld;
+    *pdf = 1 / (2 * kPi * (1 - cosThetaMax));
+}
+
 // DiffuseAreaLight::Sample_Li + Shape::Sample(ref, u, pdf) (diffuse.cpp:69-84, shape.cpp:56-74)
 template <int kFt = kFtAll>
 __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, float u0,
@@ -890,6 +1080,13 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
         *sn = v3(0, 0, 0);
         *spe = v3(0, 0, 0);
         return inf_sample_li(l, ref.p, u0, u1, wi, pdf, sp);
+    }
+    if (Ft<kFt>::sph && l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
+        sphere_sample_ref(sc.spheres[l.shape], ref, u0, u1, &p, &n, &pe, pdf);
+        if (*pdf == 0 || len2(p - ref.p) == 0) { *pdf = 0; return s3(0.f); }
+        *wi = normalize(p - ref.p);
+        *sp = p; *sn = n; *spe = pe;
+        return area_L(l, n, -*wi);
     }
     if (l.kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l.shape, u0, u1, &p, &n, &pe, pdf);
     else plane_sample(sc.planes[l.shape], u0, u1, &p, &n, &pe, pdf);
@@ -910,17 +1107,28 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
 template <int kFt = kFtAll>
 __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight& l, const SurfHit& ref, V3 wi) {
     if (Ft<kFt>::inf && l.kind == PT_LIGHT_INFINITE) return inf_pdf_li(l, wi);
+    float area = l.area;
     Ray r{offset_ray_origin(ref.p, ref.perr, ref.n, wi), wi, kInf};
     SurfHit isl;
     bool ok;
-    if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
+    if (Ft<kFt>::sph && l.kind == PT_LIGHT_DIFFUSE_SPHERE) {  // Sphere::Pdf (sphere.cpp:303-315)
+        const DevSphere& s = sc.spheres[l.shape];
+        const V3 pOrigin = offset_ray_origin(ref.p, ref.perr, ref.n, s.center - ref.p);
+        if (!(dist2(pOrigin, s.center) <= s.radius * s.radius)) {
+            const float sinThetaMax2 = s.radius * s.radius / dist2(ref.p, s.center);
+            const float cosThetaMax = sqrtf(smax(0.f, 1 - sinThetaMax2));
+            return 1 / (2 * kPi * (1 - cosThetaMax));  // UniformConePdf (sampling.cpp:132-134)
+        }
+        ok = sphere_surface(s, r, &isl);
+        area = s.area;
+    } else if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
         // Triangle::Intersect on this one triangle (tMax = Infinity).
         ok = tri_surface(sc, l.shape, r, &isl);
     } else {
         ok = plane_surface(sc.planes[l.shape], r, &isl);
     }
     if (!ok) return 0;
-    float pdf = dist2(ref.p, isl.p) / (absdot(isl.n, -wi) * l.area);
+    float pdf = dist2(ref.p, isl.p) / (absdot(isl.n, -wi) * area);
     if (__builtin_isinf(pdf)) pdf = 0.f;
     return pdf;
 }

@@ -23,6 +23,19 @@ struct DevPlane {
     M4 o2w, w2o;
 };
 
+// Sphere (src/shapes/sphere.h:50-59): the ctor's clamped members, the
+// ObjectToWorld / WorldToObject matrices and ObjectToWorld(0, 0, 0).
+struct DevSphere {
+    float radius, zmin, zmax, theta_min, theta_max, phi_max;
+    float area;        // Sphere::Area (sphere.cpp:224)
+    int ro;            // reverseOrientation (Sphere::Sample normal flip)
+    int ro_xor_sh;     // reverseOrientation ^ transformSwapsHandedness (SurfaceInteraction ctor)
+    int material;
+    int area_light;
+    V3 center;
+    M4 o2w, w2o;
+};
+
 struct DevLight {
     int kind;
     S3 L;
@@ -43,6 +56,8 @@ struct DevLight {
 // Prim record flags (word 0 .w of the 48-byte record)
 constexpr uint32_t kPrimPlane = 1u;       // AAPlaneShape (else Triangle)
 constexpr uint32_t kPrimDegenerate = 2u;  // Triangle::Intersect always rejects (triangle.cpp:309-315)
+constexpr uint32_t kPrimSphere = 4u;      // Sphere
+constexpr uint32_t kPrimAnalytic = kPrimPlane | kPrimSphere;  // record holds a shape index, not vertices
 
 struct DevScene {
     // BVH: 2 x float4 per LinearBVHNode; 3 x float4 per primitive in BVH order
@@ -57,6 +72,7 @@ struct DevScene {
     const float* UV;
     const DevPlane* planes;
     const DevPlane* portal_planes;
+    const DevSphere* spheres;
     const pt_material* mats;
     const DevLight* lights;
     int n_lights;

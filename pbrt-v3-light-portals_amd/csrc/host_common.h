@@ -2,6 +2,7 @@
 // builder and the render driver.
 #pragma once
 
+#include <cmath>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -36,6 +37,25 @@ HXF hxf_scale(float x, float y, float z);
 HXF hxf_perspective(float fov, float n, float f);
 bool hxf_swaps_handedness(const HXF& t);
 M4 to_m4(const HM4& h);
+
+// Sphere members after the ctor's clamps (shapes/sphere.h:50-59), from the
+// CreateSphereShape parameters; Area() (sphere.cpp:224).
+struct SphereMembers {
+    float radius, zmin, zmax, theta_min, theta_max, phi_max, area;
+};
+inline float clamp_to(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }  // Clamp (pbrt.h:309)
+inline SphereMembers sphere_members(const pt_sphere& s) {
+    SphereMembers m;
+    m.radius = s.radius;
+    const float zlo = smin(s.zmin, s.zmax), zhi = smax(s.zmin, s.zmax);
+    m.zmin = clamp_to(zlo, -s.radius, s.radius);
+    m.zmax = clamp_to(zhi, -s.radius, s.radius);
+    m.theta_min = std::acos(clamp_to(zlo / s.radius, -1, 1));
+    m.theta_max = std::acos(clamp_to(zhi / s.radius, -1, 1));
+    m.phi_max = (kPi / 180) * clamp_to(s.phimax, 0, 360);  // Radians (pbrt.h:329)
+    m.area = m.phi_max * m.radius * (m.zmax - m.zmin);
+    return m;
+}
 
 // Loader
 struct pt_host_scene_impl;

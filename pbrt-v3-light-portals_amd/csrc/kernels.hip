@@ -59,7 +59,7 @@ __device__ __forceinline__ void flush_stats(DevStats* s, unsigned long long cl, 
 // The 64-entry node stack lives in LDS (kStackLds entries per lane,
 // [entry][lane] layout) with a per-thread global spill for deeper trees.
 // ----------------------------------------------------------------------------
-template <bool kAny>
+template <bool kAny, bool kSph = true>
 __device__ __forceinline__ int traverse(const DevScene& sc, const float4* __restrict__ bnodes,
                                         const float4* __restrict__ bprims, Ray ray, int (*stk)[kTraceBlock],
                                         int* spill, unsigned long long* nodes, unsigned long long* prims) {
@@ -107,9 +107,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const float4* __rest
                     const uint32_t fl = __float_as_uint(r0.w);
                     float t;
                     bool ok;
-                    if (fl & kPrimPlane) {
-                        V3 ph;
-                        ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+                    if (fl & kPrimAnalytic) {
+                        ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
                     } else {
                         const float4 r2 = bprims[3 * pi + 2];
                         float b0, b1, b2;
@@ -155,7 +154,7 @@ __device__ __forceinline__ void store_ray6(float* a, uint32_t n, uint32_t slot, 
 // kLdsScene: small scenes (nodes + prim records <= kLdsSceneMax bytes) are
 // staged once per block into LDS, so the dependent node/primitive fetches of
 // the traversal are LDS reads instead of L1/L2 round trips.
-template <bool kLdsScene>
+template <bool kLdsScene, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                        const uint32_t* __restrict__ rq_count, int* spill,
                                                        DevStats* stats) {
@@ -182,7 +181,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
             const float* a = ps.rayA;
             Ray r{v3(a[slot], a[N + slot], a[2 * N + slot]), v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
                   a[6 * N + slot]};
-            int h = traverse<true>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
+            int h = traverse<true, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             ps.hitA[slot] = h >= 0 ? 1 : 0;
             ++nsh;
         } else {
@@ -190,7 +189,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
             if (kind == kRayCont) r = load_ray6(ps.ray, N, slot, kInf);
             else if (kind == kRayA) r = load_ray6(ps.rayA, N, slot, kInf);
             else r = load_ray6(ps.rayB, N, slot, kInf);
-            int h = traverse<false>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
+            int h = traverse<false, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             if (kind == kRayCont) ps.hit[slot] = h;
             else if (kind == kRayA) ps.hitA[slot] = h;
             else ps.hitB[slot] = h;
@@ -231,7 +230,7 @@ __device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray,
     return ok1 & ok2 & (tMin < ray.tmax) & (tMax > 0);
 }
 
-template <bool kLdsScene, bool kSpill>
+template <bool kLdsScene, bool kSpill, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
                                                           int refill_min, int leaf_min, int stack_rows, int* spill,
@@ -321,9 +320,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
             const uint32_t fl = __float_as_uint(r0.w);
             float t;
             bool ok;
-            if (fl & kPrimPlane) {
-                V3 ph;
-                ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+            if (fl & kPrimAnalytic) {
+                ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
             } else {
                 const float4 r2 = bprims[3 * pi + 2];
                 float b0, b1, b2;
@@ -389,7 +387,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
 // stack push is an unconditional LDS store above the top; the pop an
 // unconditional LDS load below it.  Only for BVHs whose stack fits in LDS.
 // ----------------------------------------------------------------------------
-template <bool kLdsScene>
+template <bool kLdsScene, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
                                                           int refill_min, int leaf_min, DevStats* stats) {
@@ -471,9 +469,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
                 const uint32_t fl = __float_as_uint(r0.w);
                 float t = 0;
                 bool ok;
-                if (fl & kPrimPlane) {
-                    V3 ph;
-                    ok = plane_test(sc.planes[__float_as_int(r1.w)], ray, &t, &ph);
+                if (fl & kPrimAnalytic) {
+                    ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
                 } else {
                     ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t);
                     ok &= (kind == kRayShadow) | !(fl & kPrimDegenerate);
@@ -594,15 +591,16 @@ __device__ __forceinline__ void store_s3(float* a, uint32_t n, uint32_t slot, S3
 
 // Le of whatever area light the primitive carries (SurfaceInteraction::Le,
 // interaction.cpp:148-151); the hit normal is only needed for one-sided lights.
+template <int kFt>
 __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ray, int* lightOut) {
     int mat, light;
-    prim_info(sc, prim, &mat, &light);
+    prim_info<Ft<kFt>::sph>(sc, prim, &mat, &light);
     *lightOut = light;
     if (light < 0) return s3(0.f);
     const DevLight& l = sc.lights[light];
     if (l.two_sided) return l.L;
     SurfHit si;
-    if (!surface_at(sc, prim, ray, &si)) return s3(0.f);
+    if (!surface_at<Ft<kFt>::sph>(sc, prim, ray, &si)) return s3(0.f);
     return area_L(l, si.n, -ray.d);
 }
 
@@ -620,7 +618,7 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
             const int h = ps.hitA[slot];
             if (h >= 0) {
                 int lid;
-                Li = hit_Le(sc, h, load_ray6(ps.rayA, N, slot, kInf), &lid);
+                Li = hit_Le<kFt>(sc, h, load_ray6(ps.rayA, N, slot, kInf), &lid);
             }
             const S3 f = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
             if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / nee[kNeePdf * N + slot];
@@ -635,7 +633,7 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
             S3 Li = s3(0.f);
             if (h >= 0) {
                 int lid;
-                const S3 le = hit_Le(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
+                const S3 le = hit_Le<kFt>(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
                 if (lid == nl) Li = le;
             } else if (Ft<kFt>::inf && sc.lights[nl].kind == PT_LIGHT_INFINITE) {
                 Li = inf_Le(sc.lights[nl], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
@@ -835,9 +833,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         const int hp = ps.hit[slot];
         S3 beta = load_s3(ps.beta, N, slot);
         SurfHit si;
-        bool found = hp >= 0 && surface_at(sc, hp, ray, &si);
+        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &si);
         int mat = -1, light = -1;
-        if (found) prim_info(sc, hp, &mat, &light);
+        if (found) prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
             else if (Ft<kFt>::inf)

@@ -370,6 +370,7 @@ struct pt_host_scene_impl {
     bool anyN = false, anyS = false, anyUV = false;
     std::vector<pt_triangle> tris;
     std::vector<pt_aaplane> planes;
+    std::vector<pt_sphere> spheres;
     std::vector<pt_prim> prims;
     std::vector<pt_material> materials;
     std::vector<pt_light> lights;
@@ -830,6 +831,32 @@ class Loader {
             for (double v : pp->nums) P.push_back((float)v);
             loop_subdivide(levels, idx, P, &sP, &sN, &sIdx);
             add_mesh(ps, oflags, sP, sN, {}, {}, sIdx);
+        } else if (name == "sphere") {
+            // CreateSphereShape (sphere.cpp:381-391); the renderer applies the
+            // Sphere ctor's clamps (sphere.h:50-59)
+            pt_sphere sp{};
+            sp.radius = ps.float1("radius", 1.f);
+            sp.zmin = ps.float1("zmin", -sp.radius);
+            sp.zmax = ps.float1("zmax", sp.radius);
+            sp.phimax = ps.float1("phimax", 360.f);
+            if (!(sp.radius > 0)) throw PtError(PT_ERR_UNSUPPORTED, "sphere radius must be positive");
+            sp.material = material_for(ps);
+            sp.area_light = -1;
+            sp.flags = oflags;
+            store_xf(o2w, &sp.object_to_world);
+            const int sidx = (int)out_->spheres.size();
+            if (!gs_.areaLight.empty()) {
+                if (gs_.areaLight != "diffuse" && gs_.areaLight != "area")
+                    throw PtError(PT_ERR_UNSUPPORTED, "area light \"" + gs_.areaLight + "\" on a sphere");
+                pt_light L{};
+                L.kind = PT_LIGHT_DIFFUSE_SPHERE;
+                diffuse_params(gs_.areaLightParams, &L);
+                L.shape = sidx;
+                out_->lights.push_back(L);
+                sp.area_light = (int)out_->lights.size() - 1;
+            }
+            out_->spheres.push_back(sp);
+            out_->prims.push_back(pt_prim{PT_PRIM_SPHERE, sidx});
         } else if (name == "aaplane") {
             // CreateAAPlaneShape (plane.cpp:117-128)
             V3 lo = v3(0, 0, 0), hi = v3(0, 0, 0);
@@ -1061,6 +1088,8 @@ void host_scene_fill_desc(pt_host_scene_impl* hs) {
     d.lights = hs->lights.data();
     d.n_portals = (int)hs->portals.size();
     d.portals = hs->portals.data();
+    d.n_spheres = (int)hs->spheres.size();
+    d.spheres = hs->spheres.data();
 }
 
 pt_host_scene_impl* load_pbrt_file(const char* path) {

@@ -18,6 +18,7 @@ constexpr float kPiOver4 = 0.78539816339744830961f;   // core/pbrt.h:215
 constexpr float kShadowEps = 0.0001f;                 // core/pbrt.h:209
 constexpr float kOneMinusEps = 0x1.fffffep-1f;        // core/rng.h:56-58
 constexpr float kInf = __builtin_huge_valf();
+constexpr float kMachineEps = 0x1p-24f;  // MachineEpsilon (pbrt.h:196): numeric_limits<float>::epsilon() * 0.5
 
 // gamma(n) (core/pbrt.h:294-296) evaluated in float.
 PTHD float gammaf(int n) {
@@ -147,6 +148,14 @@ PTHD V3 xf_point_err(const M4& m, V3 p, V3* err) {
     *err = gammaf(3) * v3(xs, ys, zs);
     if (wp == 1) return v3(xp, yp, zp);
     return pdiv(v3(xp, yp, zp), wp);
+}
+// Vector transform with absolute error output (transform.h:337-352)
+PTHD V3 xf_vector_err(const M4& m, V3 v, V3* err) {
+    const float g3 = gammaf(3);
+    err->x = g3 * (fabsf(m.m[0][0] * v.x) + fabsf(m.m[0][1] * v.y) + fabsf(m.m[0][2] * v.z));
+    err->y = g3 * (fabsf(m.m[1][0] * v.x) + fabsf(m.m[1][1] * v.y) + fabsf(m.m[1][2] * v.z));
+    err->z = g3 * (fabsf(m.m[2][0] * v.x) + fabsf(m.m[2][1] * v.y) + fabsf(m.m[2][2] * v.z));
+    return xf_vector(m, v);
 }
 // Point transform with incoming error (transform.h:303-334)
 PTHD V3 xf_point_err_in(const M4& m, V3 p, V3 pe, V3* err) {

@@ -177,6 +177,7 @@ struct pt_scene {
     pt::DBuf<pt_triangle> tris;
     pt::DBuf<float> P, N, S, UV, lfunc, lcdf, tri_area, perm_c0;
     pt::DBuf<pt::DevPlane> planes, pplanes;
+    pt::DBuf<pt::DevSphere> spheres;
     pt::DBuf<pt_material> mats;
     pt::DBuf<pt::DevLight> lights;
     pt::DBuf<uint16_t> perm;
@@ -197,6 +198,7 @@ struct pt_scene {
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
+    bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int refill_min = 64;         // idle lanes that trigger a refill (64: whole-wave refill)
@@ -222,6 +224,7 @@ static int scene_features(const pt_scene_desc* d) {
     }
     for (int i = 0; i < d->n_lights; ++i)
         if (d->lights[i].kind == PT_LIGHT_INFINITE) f |= kFtInfinite;
+    if (d->n_spheres > 0) f |= kFtSphere;
     return f;
 }
 
@@ -231,17 +234,36 @@ template <int kFt>
 static ShadeKernel shade_kernel_ft(int variant) {
     return variant == 4 ? k_shade_w4<kFt> : (variant == 3 ? k_shade_w3<kFt> : k_shade<kFt>);
 }
+// Instantiated feature sets: all-matte, + infinite light, + spheres, + both,
+// everything.  Other combinations take the full kernel.
 static ShadeKernel shade_kernel(int variant, int features) {
     switch (features & kFtAll) {
         case 0: return shade_kernel_ft<0>(variant);
-        case 1: return shade_kernel_ft<1>(variant);
-        case 2: return shade_kernel_ft<2>(variant);
-        case 3: return shade_kernel_ft<3>(variant);
-        case 4: return shade_kernel_ft<4>(variant);
-        case 5: return shade_kernel_ft<5>(variant);
-        case 6: return shade_kernel_ft<6>(variant);
-        default: return shade_kernel_ft<7>(variant);
+        case kFtInfinite: return shade_kernel_ft<kFtInfinite>(variant);
+        case kFtSphere: return shade_kernel_ft<kFtSphere>(variant);
+        case kFtInfinite | kFtSphere: return shade_kernel_ft<kFtInfinite | kFtSphere>(variant);
+        default: return shade_kernel_ft<kFtAll>(variant);
     }
+}
+
+using TraceNbKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, DevStats*);
+static TraceNbKernel trace_nb_kernel(bool lds, bool sph) {
+    return lds ? (sph ? k_trace_nb<true, true> : k_trace_nb<true, false>)
+               : (sph ? k_trace_nb<false, true> : k_trace_nb<false, false>);
+}
+using TracePtKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, int*,
+                               DevStats*);
+static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
+    if (lds) {
+        if (spill) return sph ? k_trace_pt<true, true, true> : k_trace_pt<true, true, false>;
+        return sph ? k_trace_pt<true, false, true> : k_trace_pt<true, false, false>;
+    }
+    if (spill) return sph ? k_trace_pt<false, true, true> : k_trace_pt<false, true, false>;
+    return sph ? k_trace_pt<false, false, true> : k_trace_pt<false, false, false>;
+}
+using TraceKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, int*, DevStats*);
+static TraceKernel trace_kernel(bool lds, bool sph) {
+    return lds ? (sph ? k_trace<true, true> : k_trace<true, false>) : (sph ? k_trace<false, true> : k_trace<false, false>);
 }
 
 // InfiniteAreaLight ctor + Preprocess (infinite.cpp:43-83): LightToWorld,
@@ -299,6 +321,9 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
             if (p.index < 0 || p.index >= d->n_triangles) throw PtError(PT_ERR_INVALID_ARG, "bad triangle prim");
         } else if (p.kind == PT_PRIM_AAPLANE) {
             if (p.index < 0 || p.index >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad plane prim");
+        } else if (p.kind == PT_PRIM_SPHERE) {
+            if (p.index < 0 || p.index >= d->n_spheres || !d->spheres)
+                throw PtError(PT_ERR_INVALID_ARG, "bad sphere prim");
         } else
             throw PtError(PT_ERR_INVALID_ARG, "bad prim kind");
     }
@@ -314,6 +339,12 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         if (p.axis < 0 || p.axis > 2) throw PtError(PT_ERR_INVALID_ARG, "bad plane axis");
         if (p.material < 0 || p.material >= d->n_materials) throw PtError(PT_ERR_INVALID_ARG, "bad material index");
     }
+    for (int i = 0; i < d->n_spheres; ++i) {
+        const pt_sphere& sp = d->spheres[i];
+        if (!(sp.radius > 0)) throw PtError(PT_ERR_INVALID_ARG, "sphere radius must be positive");
+        if (sp.material < 0 || sp.material >= d->n_materials) throw PtError(PT_ERR_INVALID_ARG, "bad material index");
+        if (sp.area_light >= d->n_lights) throw PtError(PT_ERR_INVALID_ARG, "bad light index");
+    }
     for (int i = 0; i < d->n_materials; ++i) {
         int k = d->materials[i].kind;
         if (k < PT_MAT_NONE || k > PT_MAT_PLASTIC) throw PtError(PT_ERR_UNSUPPORTED, "unsupported material kind");
@@ -328,6 +359,8 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         const pt_light& l = d->lights[i];
         if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
             if (l.shape < 0 || l.shape >= d->n_triangles) throw PtError(PT_ERR_INVALID_ARG, "bad light shape");
+        } else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
+            if (l.shape < 0 || l.shape >= d->n_spheres) throw PtError(PT_ERR_INVALID_ARG, "bad sphere light shape");
         } else if (l.kind == PT_LIGHT_PORTAL_AREA) {
             if (l.shape < 0 || l.shape >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad portal light shape");
             if (l.n_portals < 0 || l.n_portals > kMaxPortals || l.first_portal < 0 ||
@@ -359,6 +392,8 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         V3 a = v3(0, 0, 0), b = a, c = a;
         if (p.kind == PT_PRIM_AAPLANE) {
             flags = kPrimPlane;
+        } else if (p.kind == PT_PRIM_SPHERE) {
+            flags = kPrimSphere;
         } else {
             const pt_triangle& t = d->triangles[p.index];
             a = Pv(t.v[0]); b = Pv(t.v[1]); c = Pv(t.v[2]);
@@ -429,6 +464,24 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
                                     (p.flags & PT_TRI_SWAPS_HANDEDNESS) != 0, p.object_to_world, p.material,
                                     p.area_light));
     }
+    std::vector<DevSphere> spheres;
+    for (int i = 0; i < d->n_spheres; ++i) {
+        const pt_sphere& sp = d->spheres[i];
+        const SphereMembers sm = sphere_members(sp);
+        DevSphere ds{};
+        ds.radius = sm.radius; ds.zmin = sm.zmin; ds.zmax = sm.zmax;
+        ds.theta_min = sm.theta_min; ds.theta_max = sm.theta_max; ds.phi_max = sm.phi_max;
+        ds.area = sm.area;
+        const bool ro = (sp.flags & PT_TRI_REVERSE_ORIENTATION) != 0, sh = (sp.flags & PT_TRI_SWAPS_HANDEDNESS) != 0;
+        ds.ro = ro ? 1 : 0;
+        ds.ro_xor_sh = (ro != sh) ? 1 : 0;
+        ds.material = sp.material;
+        ds.area_light = sp.area_light;
+        std::memcpy(ds.o2w.m, sp.object_to_world.m, 64);
+        std::memcpy(ds.w2o.m, sp.object_to_world.minv, 64);
+        ds.center = xf_point(ds.o2w, v3(0, 0, 0));
+        spheres.push_back(ds);
+    }
     std::vector<DevPlane> pplanes((size_t)d->n_portals);
     std::vector<DevLight> lights;
     for (int i = 0; i < d->n_lights; ++i) {
@@ -443,6 +496,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         dl.n_portals = l.n_portals;
         if (l.kind == PT_LIGHT_INFINITE) init_infinite(l, s->host_nodes, &dl);
         else if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
+        else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) dl.area = spheres[l.shape].area;
         else {
             dl.area = planes[l.shape].area;
             const pt_aaplane& lp = d->planes[l.shape];
@@ -456,6 +510,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         lights.push_back(dl);
     }
     s->planes.upload(planes);
+    s->spheres.upload(spheres);
     s->pplanes.upload(pplanes);
     s->lights.upload(lights);
     s->mats.upload(d->materials, (size_t)d->n_materials);
@@ -589,6 +644,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     ds.UV = d->UV ? s->UV.p : nullptr;
     ds.planes = s->planes.p;
     ds.portal_planes = s->pplanes.p;
+    ds.spheres = s->spheres.p;
     ds.mats = s->mats.p;
     ds.lights = s->lights.p;
     ds.n_lights = nl;
@@ -761,23 +817,22 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                         // branch-reduced persistent traversal; LDS stack of depth+1 rows
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
-                        hipLaunchKernelGGL(s->lds_scene_bytes ? k_trace_nb<true> : k_trace_nb<false>, pg,
+                        hipLaunchKernelGGL(trace_nb_kernel(s->lds_scene_bytes != 0, s->has_spheres), pg,
                                            dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0, counts + 4,
                                            s->refill_min, s->leaf_min, w.stats.p);
                     } else if (s->trace_persist) {
                         // persistent: about one resident wave set; lanes refill from counts[4]
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-                        auto kt = s->lds_scene_bytes ? (s->trace_spill ? k_trace_pt<true, true> : k_trace_pt<true, false>)
-                                                     : (s->trace_spill ? k_trace_pt<false, true> : k_trace_pt<false, false>);
+                        auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
                         const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
                         hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0,
                                            counts + 4, s->refill_min, s->leaf_min, s->stack_rows, w.spill.p,
                                            w.stats.p);
                     } else if (s->lds_scene_bytes)
-                        hipLaunchKernelGGL(k_trace<true>, tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
+                        hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
                                            ps, rq_in, counts + 0, w.spill.p, w.stats.p);
                     else
-                        hipLaunchKernelGGL(k_trace<false>, tg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
+                        hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
                                            counts + 0, w.spill.p, w.stats.p);
                     HIPCHK(hipEventRecord(e.second, stream));
                     rr.launches++;
@@ -982,6 +1037,7 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (v) s->shade_variant = std::atoi(v);
         s->features = scene_features(desc);
         if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
+        s->has_spheres = (s->features & kFtSphere) != 0;
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
         if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
         if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));

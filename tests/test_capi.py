@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ptgpu.lib().pt_abi_version() == 2
+    assert ptgpu.lib().pt_abi_version() == 3
 
 
 def test_pt_h_compiles_as_c():
@@ -35,7 +35,7 @@ def test_pt_h_compiles_as_c():
 
 def test_errors_are_status_codes(tmp_path):
     p = tmp_path / "bad.pbrt"
-    p.write_text('WorldBegin\nShape "sphere"\nWorldEnd\n')
+    p.write_text('WorldBegin\nShape "cylinder"\nWorldEnd\n')
     with pytest.raises(ptgpu.PtError) as e:
         ptgpu.HostScene(str(p))
     assert e.value.status == 3  # PT_ERR_UNSUPPORTED

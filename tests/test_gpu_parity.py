@@ -337,3 +337,50 @@ def test_loopsubdiv_render_matches_oracle(tmp_path):
     got, gst = sc.render()
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst["closest_rays"] == rst["closest_rays"]
+
+
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_sphere_traversal_bit_exact(tmp_path, any_hit):
+    """Sphere::Intersect / IntersectP (EFloat bounds, clipped and transformed
+    spheres) in the device traversal == oracle, ray for ray."""
+    from test_sphere import spheres_scene
+    hs, sc = _scene(spheres_scene(tmp_path))
+    rng = np.random.default_rng(9)
+    n = 20000
+    o = np.stack([rng.uniform(-5, 5, n), rng.uniform(-2, 5, n), rng.uniform(-6, 2, n)], 1)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d, np.full((n, 1), np.inf if not any_hit else 4.0)], 1).astype(np.float32)
+    _, order = sc.bvh()
+    got = sc.debug_trace(rays, any_hit)
+    ref = pyoracle.trace(hs.desc, rays, any_hit)
+    if not any_hit:
+        got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
+    else:
+        got = (got >= 0).astype(np.int32)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("which", ["furnace", "light", "light_power", "spheres"])
+def test_sphere_render_matches_oracle(tmp_path, which):
+    """Sphere area lights (area sampling from inside, cone sampling from
+    outside, Sphere::Pdf), clipped/transformed spheres: device == oracle."""
+    import test_sphere as ts
+    if which == "furnace":
+        path = ts.sphere_furnace(tmp_path, spp=64)
+    elif which == "light":
+        path = ts.sphere_light_scene(tmp_path, maxdepth=4, spp=32)
+    elif which == "light_power":
+        extra = 'AttributeBegin\n  Translate 3 0 6\n  AreaLightSource "area" "rgb L" [3 3 3]\n' \
+                '  Material "glass"\n  Shape "sphere" "float radius" [2]\nAttributeEnd\n'
+        path = ts.sphere_light_scene(tmp_path, maxdepth=6, spp=32, extra=extra,
+                                     strategy='"string lightsamplestrategy" "power"')
+    else:
+        path = ts.spheres_scene(tmp_path)
+    hs, sc = _scene(path)
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"{which}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst["closest_rays"] == rst["closest_rays"] and gst["shadow_rays"] == rst["shadow_rays"]
