@@ -70,7 +70,8 @@ enum pt_light_kind {
     PT_LIGHT_DIFFUSE_AREA = 0, /* DiffuseAreaLight on one triangle   src/lights/diffuse.cpp */
     PT_LIGHT_PORTAL_AREA = 1,  /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
     PT_LIGHT_INFINITE = 2,     /* InfiniteAreaLight, constant L (no "mapname")  src/lights/infinite.cpp */
-    PT_LIGHT_DIFFUSE_SPHERE = 3 /* DiffuseAreaLight on one sphere     src/lights/diffuse.cpp, shapes/sphere.cpp */
+    PT_LIGHT_DIFFUSE_SPHERE = 3, /* DiffuseAreaLight on one sphere    src/lights/diffuse.cpp, shapes/sphere.cpp */
+    PT_LIGHT_POINT = 4          /* PointLight at LightToWorld(0,0,0), L = I * scale  src/lights/point.cpp */
 };
 
 enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:12 */
@@ -170,7 +171,8 @@ typedef struct pt_light {
     int32_t first_portal; /* into portals */
     int32_t n_portals;
     int32_t n_samples;    /* Light::nSamples ("nsamples"/"samples", >= 1) */
-    pt_transform light_to_world; /* infinite: LightToWorld (CTM at the LightSource) */
+    pt_transform light_to_world; /* infinite: LightToWorld (CTM at the LightSource);
+                                    point: Translate(from) * LightToWorld */
 } pt_light;
 
 typedef struct pt_camera_desc {

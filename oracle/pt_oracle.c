@@ -377,6 +377,7 @@ typedef struct {
     int nnodes;
     Plane* planes;
     Sphere* spheres;
+    XF* light_xf;              /* per light: light_to_world */
     float* tri_area;           /* per triangle (for triangle lights) */
     /* portal planes (AAPortal::portal), per desc portal */
     Plane* portal_planes;
@@ -1913,6 +1914,13 @@ static RGB area_sample_li(const Scene* sc, const pt_light* l, const SI* ref, con
         *spErr = v3(0, 0, 0);
         return inf_sample_li(&sc->inf[l - sc->d->lights], ref, u, wi, pdf, sp);
     }
+    if (l->kind == PT_LIGHT_POINT) { /* PointLight::Sample_Li (point.cpp:41-49) */
+        V3 pl = xf_pt(&sc->light_xf[l - sc->d->lights].m, v3(0, 0, 0));
+        *wi = vnorm(vsub(pl, ref->p));
+        *pdf = 1.f;
+        *sp = pl; *sn = v3(0, 0, 0); *spErr = v3(0, 0, 0);
+        return sdivf(rgbv(l->L), dist2(pl, ref->p));
+    }
     if (l->kind == PT_LIGHT_DIFFUSE_SPHERE) { /* Sphere::Sample(ref, u, pdf) override */
         sphere_sample_ref(&sc->spheres[l->shape], ref, u, &p, &n, &pe, pdf);
         if (*pdf == 0 || vlen2(vsub(p, ref->p)) == 0) { *pdf = 0; return rgb1(0); }
@@ -1987,12 +1995,16 @@ static RGB estimate_direct_mis(const Scene* sc, const SI* it, const BSDF* bsdf, 
             Ray sr = {origin, vsub(target, origin), 1 - SHADOW_EPS};
             if (scene_intersect_p(sc, &sr, ctr)) Li = rgb1(0);
             if (!sblack(Li)) {
-                lightWeight = power_heuristic(lightPdf, scatteringPdf);
-                Ld = sadd(Ld, sdivf(smulf(smul(f, Li), lightWeight), lightPdf));
+                if (l->kind == PT_LIGHT_POINT) { /* IsDeltaLight (integrator.cpp:186-188) */
+                    Ld = sadd(Ld, sdivf(smul(f, Li), lightPdf));
+                } else {
+                    lightWeight = power_heuristic(lightPdf, scatteringPdf);
+                    Ld = sadd(Ld, sdivf(smulf(smul(f, Li), lightWeight), lightPdf));
+                }
             }
         }
     }
-    {
+    if (l->kind != PT_LIGHT_POINT) {
         int sampledType = 0;
         RGB f = bsdf_sample_f(bsdf, it->wo, &wi, uScattering, &scatteringPdf, BX_ALL & ~BX_SPECULAR, &sampledType);
         f = smulf(f, vabsdot(wi, it->sn));
@@ -2358,6 +2370,11 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     ensure_init();
     memset(sc, 0, sizeof *sc);
     sc->d = d;
+    sc->light_xf = (XF*)calloc((size_t)(d->n_lights + 1), sizeof(XF));
+    for (int i = 0; i < d->n_lights; ++i) {
+        memcpy(sc->light_xf[i].m.m, d->lights[i].light_to_world.m, 64);
+        memcpy(sc->light_xf[i].mi.m, d->lights[i].light_to_world.minv, 64);
+    }
     sc->spheres = (Sphere*)calloc((size_t)(d->n_spheres + 1), sizeof(Sphere));
     for (int i = 0; i < d->n_spheres; ++i) sphere_init(&sc->spheres[i], &d->spheres[i]);
     sc->planes = (Plane*)calloc((size_t)(d->n_planes + 1), sizeof(Plane));
@@ -2399,6 +2416,10 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
                 sc->ldist_func[i] = sy(smulf(lmap_lookup(I, .5f, .5f), PI_F * I->radius * I->radius));
                 continue;
             }
+            if (l->kind == PT_LIGHT_POINT) { /* PointLight::Power = 4 Pi I (point.cpp:51) */
+                sc->ldist_func[i] = sy(smulf(rgbv(l->L), 4 * PI_F));
+                continue;
+            }
             float area = l->kind == PT_LIGHT_DIFFUSE_AREA     ? sc->tri_area[l->shape]
                          : l->kind == PT_LIGHT_DIFFUSE_SPHERE ? sc->spheres[l->shape].area
                                                                : sc->planes[l->shape].area;
@@ -2429,7 +2450,7 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     return 0;
 }
 static void scene_free(Scene* sc) {
-    free(sc->planes); free(sc->spheres); free(sc->tri_area); free(sc->portal_planes);
+    free(sc->planes); free(sc->spheres); free(sc->light_xf); free(sc->tri_area); free(sc->portal_planes);
     free(sc->prim_kind); free(sc->prim_index); free(sc->nodes);
     free(sc->ldist_func); free(sc->ldist_cdf); free(sc->inf);
 }

@@ -1081,6 +1081,12 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
         *spe = v3(0, 0, 0);
         return inf_sample_li(l, ref.p, u0, u1, wi, pdf, sp);
     }
+    if (l.kind == PT_LIGHT_POINT) {  // PointLight::Sample_Li (point.cpp:41-49)
+        *wi = normalize(l.center - ref.p);
+        *pdf = 1.f;
+        *sp = l.center; *sn = v3(0, 0, 0); *spe = v3(0, 0, 0);
+        return l.L / dist2(l.center, ref.p);
+    }
     if (Ft<kFt>::sph && l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
         sphere_sample_ref(sc.spheres[l.shape], ref, u0, u1, &p, &n, &pe, pdf);
         if (*pdf == 0 || len2(p - ref.p) == 0) { *pdf = 0; return s3(0.f); }

@@ -783,12 +783,16 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
             a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
             a[3 * N + slot] = d.x; a[4 * N + slot] = d.y; a[5 * N + slot] = d.z;
             a[6 * N + slot] = 1 - kShadowEps;
-            const float lightWeight = power_heuristic(lightPdf, scatteringPdf);
-            put_nee3(ps, slot, kNeeF, ((f * Li) * lightWeight) / lightPdf);
+            if (l.kind == PT_LIGHT_POINT) {  // IsDeltaLight: no MIS weight (integrator.cpp:186-188)
+                put_nee3(ps, slot, kNeeF, (f * Li) / lightPdf);
+            } else {
+                const float lightWeight = power_heuristic(lightPdf, scatteringPdf);
+                put_nee3(ps, slot, kNeeF, ((f * Li) * lightWeight) / lightPdf);
+            }
             flags |= kNfA | kNfC1;
         }
     }
-    {
+    if (l.kind != PT_LIGHT_POINT) {  // BSDF sampling only for non-delta lights
         float pdf2 = scatteringPdf;
         V3 wi2 = wi;
         int sampledType = 0;

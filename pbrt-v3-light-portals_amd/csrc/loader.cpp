@@ -912,6 +912,22 @@ class Loader {
             out_->lights.push_back(L);
             return;
         }
+        if (name == "point") {
+            // CreatePointLight (point.cpp:80-88)
+            pt_light L{};
+            L.kind = PT_LIGHT_POINT;
+            float I[3] = {1, 1, 1}, sc[3] = {1, 1, 1};
+            ps.spectrum("I", I);
+            ps.spectrum("scale", sc);
+            for (int i = 0; i < 3; ++i) L.L[i] = I[i] * sc[i];
+            V3 from = v3(0, 0, 0);
+            ps.point3("from", &from);
+            L.n_samples = std::max(1, ps.int1("samples", ps.int1("nsamples", 1)));
+            L.shape = -1;
+            store_xf(hxf_mul(hxf_translate(from.x, from.y, from.z), ctm_), &L.light_to_world);
+            out_->lights.push_back(L);
+            return;
+        }
         throw PtError(PT_ERR_UNSUPPORTED, "LightSource \"" + name + "\" is outside the supported subset");
     }
 

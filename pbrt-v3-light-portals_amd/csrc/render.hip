@@ -366,7 +366,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
             if (l.n_portals < 0 || l.n_portals > kMaxPortals || l.first_portal < 0 ||
                 l.first_portal + l.n_portals > d->n_portals)
                 throw PtError(PT_ERR_INVALID_ARG, "bad portal range");
-        } else if (l.kind != PT_LIGHT_INFINITE)
+        } else if (l.kind != PT_LIGHT_INFINITE && l.kind != PT_LIGHT_POINT)
             throw PtError(PT_ERR_UNSUPPORTED, "unsupported light kind");
     }
     if (d->sampler.spp <= 0) throw PtError(PT_ERR_INVALID_ARG, "spp must be > 0");
@@ -497,6 +497,11 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         if (l.kind == PT_LIGHT_INFINITE) init_infinite(l, s->host_nodes, &dl);
         else if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
         else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) dl.area = spheres[l.shape].area;
+        else if (l.kind == PT_LIGHT_POINT) {  // pLight = LightToWorld(Point3f(0, 0, 0)) (point.h:55)
+            M4 m;
+            std::memcpy(m.m, l.light_to_world.m, 64);
+            dl.center = xf_point(m, v3(0, 0, 0));
+        }
         else {
             dl.area = planes[l.shape].area;
             const pt_aaplane& lp = d->planes[l.shape];
@@ -525,6 +530,10 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
                 const DevLight& l = lights[i];
                 if (l.kind == PT_LIGHT_INFINITE) {  // InfiniteAreaLight::Power (infinite.cpp:85-89)
                     func[i] = lum_y(lmap_triangle(l.L, .5f, .5f) * (kPi * l.radius * l.radius));
+                    continue;
+                }
+                if (l.kind == PT_LIGHT_POINT) {  // PointLight::Power (point.cpp:51)
+                    func[i] = lum_y(l.L * (4 * kPi));
                     continue;
                 }
                 S3 pw = ((l.L * (float)(l.two_sided ? 2 : 1)) * l.area) * kPi;  // DiffuseAreaLight::Power

@@ -384,3 +384,20 @@ def test_sphere_render_matches_oracle(tmp_path, which):
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst["closest_rays"] == rst["closest_rays"] and gst["shadow_rays"] == rst["shadow_rays"]
+
+
+@pytest.mark.parametrize("extra", ["", "sphere", "power"])
+def test_point_light_render_matches_oracle(tmp_path, extra):
+    """PointLight (delta light: no MIS weight, no BSDF-sampled light ray),
+    alone, next to a sphere light, and under "power" light selection."""
+    import test_sphere as ts
+    ex = ""
+    if extra:
+        ex = 'AttributeBegin\n  Translate 1 1 3\n  AreaLightSource "area" "rgb L" [2 2 2]\n' \
+             '  Shape "sphere" "float radius" [0.5]\nAttributeEnd\n'
+    hs, sc = _scene(ts.point_light_scene(tmp_path, maxdepth=5, spp=32, extra=ex,
+                                         strategy='"string lightsamplestrategy" "power"' if extra == "power" else ""))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst["closest_rays"] == rst["closest_rays"] and gst["shadow_rays"] == rst["shadow_rays"]

@@ -206,3 +206,38 @@ def test_sphere_scene_renders_in_oracle(tmp_path):
     hs = ptgpu.HostScene(spheres_scene(tmp_path))
     img, st = pyoracle.render(hs.desc, nthreads=8)
     assert np.isfinite(img).all() and img.mean() > 0
+
+
+# ---- PointLight (lights/point.cpp) -------------------------------------------------------------
+
+def point_light_scene(tmp_path, h=2.0, I=5.0, maxdepth=1, spp=16, extra="", strategy=""):
+    return write(tmp_path, "point.pbrt", f"""LookAt 0 0 1  0 0 0  0 1 0
+Camera "perspective" "float fov" [0.5]
+PixelFilter "box" "float xwidth" [0.5] "float ywidth" [0.5]
+Film "image" "integer xresolution" [8] "integer yresolution" [8]
+Sampler "halton" "integer pixelsamples" [{spp}]
+Integrator "path" "integer maxdepth" [{maxdepth}] {strategy}
+WorldBegin
+AttributeBegin
+  Translate 0.5 0 0
+  LightSource "point" "rgb I" [{I} {I} {I}] "point from" [-0.5 0 {h}]
+AttributeEnd
+AttributeBegin
+  Material "matte" "rgb Kd" [0.5 0.5 0.5]
+  Shape "trianglemesh" "point P" [-50 -50 0  50 -50 0  50 50 0  -50 50 0] "integer indices" [0 1 2 0 2 3]
+AttributeEnd
+{extra}
+WorldEnd
+""")
+
+
+def test_point_light_known_answer(tmp_path):
+    """Lambertian floor straight below a point light: L_o = Kd/pi * I / h^2
+    (PointLight::Sample_Li, delta light: no MIS, no BSDF sample)."""
+    h, I = 2.0, 5.0
+    hs = ptgpu.HostScene(point_light_scene(tmp_path, h=h, I=I))
+    img, st = pyoracle.render(hs.desc, nthreads=8)
+    expect = 0.5 / math.pi * I / h ** 2
+    assert abs(float(img.mean()) - expect) < 1e-3 * expect, (float(img.mean()), expect)
+    # one shadow ray per sample and no BSDF-sampled light ray; closest: camera + continuation
+    assert st["shadow_rays"] == 8 * 8 * 16 and st["closest_rays"] == 2 * 8 * 8 * 16
