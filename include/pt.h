@@ -12,13 +12,16 @@
  *   PathIntegrator::Li(...)  src/integrators/path.cpp:64-189  (device wavefront, no host call)
  *   CreatePathIntegrator(ParamSet, Sampler, Camera)         pt_integrator_desc
  *     src/integrators/path.cpp:191-214
+ *   CreateDirectLightingIntegrator                          pt_integrator_desc (kind DIRECT)
+ *     src/integrators/directlighting.cpp:86-118
  *   CreateHaltonSampler  src/samplers/halton.cpp:133-139    pt_sampler_desc
  *   CreatePerspectiveCamera  src/cameras/perspective.cpp    pt_camera_desc
  *   CreateFilm / CreateBoxFilter / CreateGaussianFilter     pt_film_desc
  *     src/core/film.cpp:213-252, src/filters/{box,gaussian}.cpp
  *   Scene{aggregate, lights}  src/core/scene.h:50-80         pt_scene_desc + pt_scene_create
  *   CreateBVHAccelerator  src/accelerators/bvh.cpp:740-760   built inside pt_scene_create
- *   MakeShapes "trianglemesh"/"aaplane"  src/core/api.cpp:432-546   pt_triangle / pt_aaplane
+ *   MakeShapes "trianglemesh"/"plymesh"/"loopsubdiv"/"sphere"/"aaplane"
+ *     src/core/api.cpp:432-546                              pt_triangle / pt_sphere / pt_aaplane
  *   MakeAreaLight "diffuse"/"portal"  src/core/api.cpp:768-786      pt_light
  *   CreateAAPortal  src/lights/portal_arealight.cpp:245-300          pt_light + pt_portal
  *   pbrtParseFile  src/core/parser.cpp:1094                 pt_load_pbrt (host scene loader)
@@ -83,6 +86,15 @@ enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:
 enum pt_filter_kind { PT_FILTER_BOX = 0, PT_FILTER_GAUSSIAN = 1 };
 
 enum pt_light_sample_strategy { PT_LIGHTS_UNIFORM = 0, PT_LIGHTS_POWER = 1 };
+
+enum pt_integrator_kind {
+    PT_INTEGRATOR_PATH = 0,    /* PathIntegrator            src/integrators/path.cpp */
+    PT_INTEGRATOR_DIRECT = 1   /* DirectLightingIntegrator  src/integrators/directlighting.cpp */
+};
+enum pt_direct_strategy {      /* LightStrategy  src/integrators/directlighting.h */
+    PT_DIRECT_ALL = 0,         /* "all": UniformSampleAllLights with per-light sample arrays */
+    PT_DIRECT_ONE = 1          /* "one": UniformSampleOneLight (uniform choice) */
+};
 
 /* Transform (src/core/transform.h): m and its stored inverse mInv, row-major. */
 typedef struct pt_transform {
@@ -207,6 +219,8 @@ typedef struct pt_integrator_desc {
     int32_t light_strategy;        /* pt_light_sample_strategy */
     int32_t has_pixel_bounds;
     int32_t pixel_bounds[4];       /* x0, x1, y0, y1 as in the "pixelbounds" param */
+    int32_t kind;                  /* pt_integrator_kind */
+    int32_t direct_strategy;       /* pt_direct_strategy (kind == PT_INTEGRATOR_DIRECT) */
 } pt_integrator_desc;
 
 typedef struct pt_scene_desc {

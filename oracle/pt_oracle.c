@@ -401,6 +401,10 @@ typedef struct {
     int spp;
     int s_begin, s_end;  /* camera-sample index range rendered per pixel */
     int max_depth;
+    int integrator;            /* pt_integrator_kind */
+    int dl_strategy;           /* pt_direct_strategy */
+    int n2D;                   /* DirectLighting "all": requested 2D arrays */
+    int* sizes2D;
     float rr_threshold;
     int pix_x0, pix_y0, pix_x1, pix_y1; /* integrator pixelBounds */
 } Scene;
@@ -564,14 +568,49 @@ static float halton_dim(const Halton* h, int64_t index, int dim) { /* halton.cpp
     return scrambled_radical_inverse(dim, (uint64_t)index, g_perms + g_prime_sums[dim]);
 }
 
-/* GlobalSampler (sampler.cpp:137-196) -- PathIntegrator requests no sample
- * arrays, so arrayStartDim == arrayEndDim == 5 and no dimension is skipped. */
-typedef struct { const Halton* h; int64_t index; int dim; } Samp;
-static float get1d(Samp* s) { return halton_dim(s->h, s->index, s->dim++); }
+/* GlobalSampler (sampler.cpp:137-196).  PathIntegrator requests no sample
+ * arrays (arrayEndDim == arrayStartDim == 5: nothing is skipped); the
+ * DirectLightingIntegrator's "all" strategy requests 2D arrays, which occupy
+ * dimensions [5, arrayEndDim) and are drawn from the pixel's sample indices
+ * s*n .. s*n+n-1 (StartPixel, sampler.cpp:137-162). */
+#define ARRAY_START_DIM 5 /* sampler.h:122 */
+typedef struct {
+    const Halton* h;
+    int64_t index;             /* GetIndexForSample(s) */
+    int dim;
+    int64_t pixOff;            /* GetIndexForSample(0) */
+    int s;                     /* currentPixelSampleIndex */
+    int arrayEndDim;
+    int n2D, off2D;            /* requested 2D arrays / array2DOffset */
+    const int* sizes2D;
+    int overflow;              /* a dimension past the prime table was requested */
+} Samp;
+static float samp_dim(Samp* s, int64_t index, int dim) {
+    if (dim >= PRIME_TABLE_SIZE) { s->overflow = 1; return 0.5f; } /* the reference CHECK-fails here */
+    return halton_dim(s->h, index, dim);
+}
+static float get1d(Samp* s) {
+    if (s->dim >= ARRAY_START_DIM && s->dim < s->arrayEndDim) s->dim = s->arrayEndDim;
+    return samp_dim(s, s->index, s->dim++);
+}
 static void get2d(Samp* s, float* u) {
-    u[0] = halton_dim(s->h, s->index, s->dim);
-    u[1] = halton_dim(s->h, s->index, s->dim + 1);
+    if (s->dim + 1 >= ARRAY_START_DIM && s->dim < s->arrayEndDim) s->dim = s->arrayEndDim;
+    u[0] = samp_dim(s, s->index, s->dim);
+    u[1] = samp_dim(s, s->index, s->dim + 1);
     s->dim += 2;
+}
+/* Sampler::Get2DArray (sampler.cpp:89-94): the next requested array, or NULL */
+static int get2d_array(Samp* s, int n, float* out) {
+    if (s->off2D == s->n2D) return 0;
+    int i = s->off2D++;
+    int dim = ARRAY_START_DIM + 2 * i;
+    for (int k = 0; k < n; ++k) {
+        int64_t idx = s->pixOff + (int64_t)(s->s * n + k) * s->h->stride;
+        out[2 * k] = samp_dim(s, idx, dim);
+        out[2 * k + 1] = samp_dim(s, idx, dim + 1);
+    }
+    (void)s->sizes2D;
+    return 1;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1239,7 +1278,7 @@ static int bb_hit(const BB* b, const Ray* ray, V3 invDir, const int* neg) {
     return (tMin < ray->tMax) && (tMax > 0);
 }
 
-typedef struct { uint64_t closest, shadow, nodes, prims, camera; } Counters;
+typedef struct { uint64_t closest, shadow, nodes, prims, camera, dim_overflow; } Counters;
 
 /* Scene::Intersect -> BVHAccel::Intersect (scene.cpp:45-49, bvh.cpp:662-700) */
 static int scene_intersect(const Scene* sc, Ray* ray, SI* si, Counters* ctr) {
@@ -1449,7 +1488,7 @@ static RGB frConductor(float cosThetaI, RGB etai, RGB etat, RGB k) {
 #define BX_GLOSSY 8
 #define BX_SPECULAR 16
 #define BX_ALL 31
-enum { LB_LAMBERT = 1, LB_MFREFL, LB_MFTRANS, LB_FRESNELSPEC, LB_SPECREFL };
+enum { LB_LAMBERT = 1, LB_MFREFL, LB_MFTRANS, LB_FRESNELSPEC, LB_SPECREFL, LB_SPECTRANS };
 enum { FR_NOOP = 0, FR_CONDUCTOR, FR_DIELECTRIC };
 typedef struct {
     int kind, type, fres;
@@ -1588,6 +1627,17 @@ static RGB lobe_sample(const Lobe* l, V3 wo, V3* wi, const float* u, float* pdf,
             *pdf = 1;
             return sdivf(smul(fresnel_eval(l, wi->z), l->R), fabsf(wi->z));
         }
+        case LB_SPECTRANS: { /* SpecularTransmission::Sample_f (reflection.cpp:183-199) */
+            int entering = wo.z > 0;
+            float etaI = entering ? l->etaA : l->etaB;
+            float etaT = entering ? l->etaB : l->etaA;
+            V3 n = vdot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1); /* Faceforward(n, wo) */
+            if (!refract(wo, n, etaI / etaT, wi)) return rgb1(0);
+            *pdf = 1;
+            RGB ft = smul(l->R, ssub(rgb1(1.), rgb1(frDielectric(wi->z, l->etaA, l->etaB))));
+            ft = smulf(ft, (etaI * etaI) / (etaT * etaT)); /* TransportMode::Radiance */
+            return sdivf(ft, fabsf(wi->z));
+        }
         case LB_FRESNELSPEC: { /* FresnelSpecular::Sample_f (reflection.cpp:520-554) */
             float F = frDielectric(wo.z, l->etaA, l->etaB);
             if (u[0] < F) {
@@ -1621,9 +1671,12 @@ static RGB clamp0(RGB r) { /* Spectrum::Clamp() */
     for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] < 0 ? 0 : (r.c[i] > INFINITY ? INFINITY : r.c[i]);
     return r;
 }
-/* Material::ComputeScatteringFunctions(si, arena, Radiance, allowMultipleLobes = true)
- * + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength. */
-static void make_bsdf(const pt_material* m, const SI* si, float wvl0, BSDF* b) {
+/* Material::ComputeScatteringFunctions(si, arena, Radiance, allowMultipleLobes)
+ * + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength.
+ * PathIntegrator passes allowMultipleLobes = true (path.cpp:106), the
+ * DirectLightingIntegrator the default false (directlighting.cpp:72): smooth
+ * glass is then SpecularReflection + SpecularTransmission (glass.cpp:62-83). */
+static void make_bsdf(const pt_material* m, const SI* si, float wvl0, int multi, BSDF* b) {
     b->ns = si->sn; b->ng = si->n;
     b->ss = vnorm(si->sdpdu);
     b->ts = vcross(b->ns, b->ss);
@@ -1671,10 +1724,21 @@ static void make_bsdf(const pt_material* m, const SI* si, float wvl0, BSDF* b) {
             b->eta = eta;
             RGB R = clamp0(rgbv(m->kr)), T = clamp0(rgbv(m->kt));
             if (sblack(R) && sblack(T)) break;
-            if (m->specular) {
+            if (m->specular && multi) {
                 add_lobe(b, LB_FRESNELSPEC, BX_REFLECTION | BX_TRANSMISSION | BX_SPECULAR, R);
                 b->lb[0].etaA = 1.f; b->lb[0].etaB = eta;
                 b->lb[0].T = T;
+            } else if (m->specular) {
+                if (!sblack(R)) {
+                    add_lobe(b, LB_SPECREFL, BX_REFLECTION | BX_SPECULAR, R);
+                    Lobe* l = &b->lb[b->n - 1];
+                    l->fres = FR_DIELECTRIC; l->fetaI = 1.f; l->fetaT = eta;
+                }
+                if (!sblack(T)) {
+                    add_lobe(b, LB_SPECTRANS, BX_TRANSMISSION | BX_SPECULAR, T);
+                    Lobe* l = &b->lb[b->n - 1];
+                    l->etaA = 1.f; l->etaB = eta;
+                }
             } else {
                 if (!sblack(R)) {
                     add_lobe(b, LB_MFREFL, BX_REFLECTION | BX_GLOSSY, R);
@@ -2151,7 +2215,7 @@ static RGB path_li(const Scene* sc, Ray ray, float wvl0, Samp* smp, Counters* ct
             continue;
         }
         BSDF bsdf;
-        make_bsdf(mat, &isect, wvl0, &bsdf);
+        make_bsdf(mat, &isect, wvl0, 1, &bsdf);
         if (bsdf_num(&bsdf, BX_ALL & ~BX_SPECULAR) > 0) {
             /* UniformSampleOneLight (integrator.cpp:100-122) */
             RGB Ld = rgb1(0);
@@ -2310,6 +2374,94 @@ static void tile_add_sample(const Scene* sc, FilmTile* t, float fx, float fy, RG
         }
 }
 
+/* ------------------------------------------------------------------------ */
+/* integrators/directlighting.cpp                                           */
+/* ------------------------------------------------------------------------ */
+static RGB dl_estimate(const Scene* sc, const SI* it, const BSDF* bsdf, const float* uScattering, int lightIdx,
+                       const float* uLight, Counters* ctr) { /* EstimateDirect (integrator.cpp:124-135) dispatch */
+    if (sc->d->lights[lightIdx].kind == PT_LIGHT_PORTAL_AREA)
+        return estimate_direct_portal(sc, it, bsdf, uScattering, lightIdx, ctr);
+    return estimate_direct_mis(sc, it, bsdf, uScattering, lightIdx, uLight, ctr);
+}
+/* UniformSampleAllLights (integrator.cpp:69-98) */
+static RGB dl_sample_all(const Scene* sc, const SI* it, const BSDF* bsdf, Samp* smp, Counters* ctr) {
+    RGB L = rgb1(0);
+    for (int j = 0; j < sc->d->n_lights; ++j) {
+        int n = sc->d->lights[j].n_samples;
+        float* uLA = (float*)malloc(sizeof(float) * 2 * (size_t)n);
+        float* uSA = (float*)malloc(sizeof(float) * 2 * (size_t)n);
+        int okL = get2d_array(smp, n, uLA);
+        int okS = get2d_array(smp, n, uSA);
+        if (!okL || !okS) {
+            float uLight[2], uScattering[2];
+            get2d(smp, uLight);
+            get2d(smp, uScattering);
+            L = sadd(L, dl_estimate(sc, it, bsdf, uScattering, j, uLight, ctr));
+        } else {
+            RGB Ld = rgb1(0);
+            for (int k = 0; k < n; ++k) Ld = sadd(Ld, dl_estimate(sc, it, bsdf, uSA + 2 * k, j, uLA + 2 * k, ctr));
+            L = sadd(L, sdivf(Ld, (float)n));
+        }
+        free(uLA); free(uSA);
+    }
+    return L;
+}
+/* UniformSampleOneLight without a light distribution (integrator.cpp:100-122) */
+static RGB dl_sample_one(const Scene* sc, const SI* it, const BSDF* bsdf, Samp* smp, Counters* ctr) {
+    int nLights = sc->d->n_lights;
+    if (nLights == 0) return rgb1(0);
+    int lightNum = (int)(get1d(smp) * nLights);
+    if (lightNum > nLights - 1) lightNum = nLights - 1;
+    float lightPdf = (float)1 / nLights;
+    float uLight[2], uScattering[2];
+    get2d(smp, uLight);
+    get2d(smp, uScattering);
+    return sdivf(dl_estimate(sc, it, bsdf, uScattering, lightNum, uLight, ctr), lightPdf);
+}
+static RGB dl_li(const Scene* sc, Ray ray, float wvl0, Samp* smp, int depth, Counters* ctr);
+/* SamplerIntegrator::SpecularReflect / SpecularTransmit (integrator.cpp:639-770), no differentials */
+static RGB dl_specular(const Scene* sc, const SI* isect, const BSDF* bsdf, int type, float wvl0, Samp* smp, int depth,
+                       Counters* ctr) {
+    float u[2];
+    get2d(smp, u);
+    V3 wi = v3(0, 0, 0);
+    float pdf = 0;
+    int sampled = 0;
+    RGB f = bsdf_sample_f(bsdf, isect->wo, &wi, u, &pdf, type | BX_SPECULAR, &sampled);
+    if (pdf > 0.f && !sblack(f) && vabsdot(wi, isect->sn) != 0.f) {
+        Ray rd = spawn_ray(isect->p, isect->pError, isect->n, wi);
+        RGB Li = dl_li(sc, rd, wvl0, smp, depth + 1, ctr);
+        return sdivf(smulf(smul(f, Li), vabsdot(wi, isect->sn)), pdf);
+    }
+    return rgb1(0);
+}
+/* DirectLightingIntegrator::Li (directlighting.cpp:58-84) */
+static RGB dl_li(const Scene* sc, Ray ray, float wvl0, Samp* smp, int depth, Counters* ctr) {
+    RGB L = rgb1(0);
+    SI isect;
+    if (!scene_intersect(sc, &ray, &isect, ctr)) {
+        for (int li = 0; li < sc->d->n_lights; ++li) /* Light::Le: only the infinite light emits */
+            if (sc->d->lights[li].kind == PT_LIGHT_INFINITE) L = sadd(L, inf_Le(&sc->inf[li], ray.d));
+        return L;
+    }
+    int mi = si_material(sc, &isect);
+    const pt_material* mat = (mi >= 0) ? &sc->d->materials[mi] : NULL;
+    if (!mat || mat->kind == PT_MAT_NONE)
+        return dl_li(sc, spawn_ray(isect.p, isect.pError, isect.n, ray.d), wvl0, smp, depth, ctr);
+    BSDF bsdf;
+    make_bsdf(mat, &isect, wvl0, 0, &bsdf);
+    L = sadd(L, si_Le(sc, &isect, isect.wo));
+    if (sc->d->n_lights > 0) {
+        if (sc->dl_strategy == PT_DIRECT_ALL) L = sadd(L, dl_sample_all(sc, &isect, &bsdf, smp, ctr));
+        else L = sadd(L, dl_sample_one(sc, &isect, &bsdf, smp, ctr));
+    }
+    if (depth + 1 < sc->max_depth) {
+        L = sadd(L, dl_specular(sc, &isect, &bsdf, BX_REFLECTION, wvl0, smp, depth, ctr));
+        L = sadd(L, dl_specular(sc, &isect, &bsdf, BX_TRANSMISSION, wvl0, smp, depth, ctr));
+    }
+    return L;
+}
+
 static void render_tile(const Scene* sc, const Halton* h, int tx, int ty, FilmTile* ft, Counters* ctr) {
     const int ts = 16;
     int x0 = sc->sb_x0 + tx * ts, y0 = sc->sb_y0 + ty * ts;
@@ -2331,7 +2483,12 @@ static void render_tile(const Scene* sc, const Halton* h, int tx, int ty, FilmTi
             if (!(x >= sc->pix_x0 && x < sc->pix_x1 && y >= sc->pix_y0 && y < sc->pix_y1)) continue;
             int64_t off = halton_pixel_offset(h, x, y);
             for (int s = sc->s_begin; s < sc->s_end; ++s) {
-                Samp smp = {h, off + (int64_t)s * h->stride, 0};
+                Samp smp;
+                memset(&smp, 0, sizeof smp);
+                smp.h = h; smp.index = off + (int64_t)s * h->stride; smp.dim = 0;
+                smp.pixOff = off; smp.s = s;
+                smp.n2D = sc->n2D; smp.sizes2D = sc->sizes2D;
+                smp.arrayEndDim = ARRAY_START_DIM + 2 * sc->n2D;
                 float uf[2], ul[2];
                 get2d(&smp, uf);                 /* pFilm */
                 float fx = (float)x + uf[0], fy = (float)y + uf[1];
@@ -2342,7 +2499,9 @@ static void render_tile(const Scene* sc, const Halton* h, int tx, int ty, FilmTi
                 float wvl0 = (float)400 + (float)300 * uw;
                 Ray r = camera_ray(sc, fx, fy, ul);
                 ctr->camera++;
-                RGB L = path_li(sc, r, wvl0, &smp, ctr);
+                RGB L = sc->integrator == PT_INTEGRATOR_DIRECT ? dl_li(sc, r, wvl0, &smp, 0, ctr)
+                                                               : path_li(sc, r, wvl0, &smp, ctr);
+                if (smp.overflow) ctr->dim_overflow++;
                 /* radiance sanitiser (integrator.cpp:592-613) */
                 if (snan(L)) L = rgb1(0);
                 else if (sy(L) < -1e-5) L = rgb1(0);
@@ -2435,6 +2594,17 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     sc->s_begin = 0;
     sc->s_end = d->sampler.spp;
     sc->max_depth = d->integrator.max_depth;
+    sc->integrator = d->integrator.kind;
+    sc->dl_strategy = d->integrator.direct_strategy;
+    sc->n2D = 0;
+    sc->sizes2D = NULL;
+    if (sc->integrator == PT_INTEGRATOR_DIRECT && sc->dl_strategy == PT_DIRECT_ALL && d->n_lights > 0) {
+        /* DirectLightingIntegrator::Preprocess (directlighting.cpp:43-56): per depth, per
+         * light, two arrays of RoundCount(nSamples) = nSamples (GlobalSampler) */
+        sc->n2D = 2 * d->n_lights * sc->max_depth;
+        sc->sizes2D = (int*)malloc(sizeof(int) * (size_t)(sc->n2D + 1));
+        for (int i = 0; i < sc->n2D; ++i) sc->sizes2D[i] = d->lights[(i / 2) % d->n_lights].n_samples;
+    }
     sc->rr_threshold = d->integrator.rr_threshold;
     sc->pix_x0 = sc->sb_x0; sc->pix_y0 = sc->sb_y0; sc->pix_x1 = sc->sb_x1; sc->pix_y1 = sc->sb_y1;
     if (d->integrator.has_pixel_bounds) {
@@ -2450,7 +2620,7 @@ static int scene_setup(Scene* sc, const pt_scene_desc* d) {
     return 0;
 }
 static void scene_free(Scene* sc) {
-    free(sc->planes); free(sc->spheres); free(sc->light_xf); free(sc->tri_area); free(sc->portal_planes);
+    free(sc->planes); free(sc->spheres); free(sc->light_xf); free(sc->sizes2D); free(sc->tri_area); free(sc->portal_planes);
     free(sc->prim_kind); free(sc->prim_index); free(sc->nodes);
     free(sc->ldist_func); free(sc->ldist_cdf); free(sc->inf);
 }
@@ -2479,7 +2649,7 @@ static void* worker(void* arg) {
     }
     pthread_mutex_lock(&p->mu);
     p->total.closest += c.closest; p->total.shadow += c.shadow; p->total.nodes += c.nodes;
-    p->total.prims += c.prims; p->total.camera += c.camera;
+    p->total.prims += c.prims; p->total.camera += c.camera; p->total.dim_overflow += c.dim_overflow;
     pthread_mutex_unlock(&p->mu);
     return NULL;
 }
@@ -2566,7 +2736,7 @@ static int render_common(const pt_scene_desc* desc, float* rgb_out, float* accum
     free(pool.tiles);
     pthread_mutex_destroy(&pool.mu);
     scene_free(&sc);
-    return 0;
+    return pool.total.dim_overflow ? 3 : 0; /* 3: Halton dimension past the prime table */
 }
 
 int oracle_render(const pt_scene_desc* desc, float* rgb_out, int nthreads, int max_tiles, oracle_stats* stats) {
@@ -2584,11 +2754,11 @@ void oracle_set_trig(int correctly_rounded) { g_cr_trig = correctly_rounded; }
 
 /* BSDF of a material in the shading frame ns = ng = (0,0,1), ss = (1,0,0):
  * f and pdf for (wo, wi), and Sample_f for (wo, u).  Known-answer hook. */
-static void local_bsdf(const pt_material* m, BSDF* b) {
+static void local_bsdf(const pt_material* m, int multi, BSDF* b) {
     SI si;
     memset(&si, 0, sizeof si);
     si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
-    make_bsdf(m, &si, 550.f, b);
+    make_bsdf(m, &si, 550.f, multi, b);
 }
 /* Batched BSDF hook with the layout of the product's pt_debug_bsdf: per record
  * in8 = wo[3], wi[3], u0, u1 -> out8 = f[3], pdf, sampled wi[3], sampled pdf
@@ -2596,7 +2766,7 @@ static void local_bsdf(const pt_material* m, BSDF* b) {
 int oracle_bsdf_batch(const pt_scene_desc* d, int mat, int n, const float* in8, float* out8) {
     BSDF b;
     if (!d || mat < 0 || mat >= d->n_materials) return 1;
-    local_bsdf(&d->materials[mat], &b);
+    local_bsdf(&d->materials[mat], d->integrator.kind != PT_INTEGRATOR_DIRECT, &b);
     for (int i = 0; i < n; ++i) {
         const float* a = in8 + 8 * i;
         float* o = out8 + 8 * i;

@@ -81,11 +81,18 @@ def film_size(desc: int) -> Tuple[int, int]:
     return w.value, h.value
 
 
+def _chk(rc: int) -> None:
+    if rc == 3:
+        raise RuntimeError("oracle: Halton dimension past the prime table (the reference CHECK-fails)")
+    if rc != 0:
+        raise RuntimeError(f"oracle: error {rc}")
+
+
 def render(desc: int, nthreads: int = 1, max_tiles: int = -1) -> Tuple[np.ndarray, dict]:
     w, h = film_size(desc)
     rgb = np.zeros((h, w, 3), np.float32)
     st = oracle_stats()
-    lib().oracle_render(ctypes.c_void_p(desc), rgb.ctypes.data, nthreads, max_tiles, ctypes.byref(st))
+    _chk(lib().oracle_render(ctypes.c_void_p(desc), rgb.ctypes.data, nthreads, max_tiles, ctypes.byref(st)))
     return rgb, st.as_dict()
 
 
@@ -93,8 +100,8 @@ def render_accum(desc: int, nthreads: int = 1, tile_offset: int = 0, tile_stride
     w, h = film_size(desc)
     acc = np.zeros((h, w, 4), np.float32)
     st = oracle_stats()
-    lib().oracle_render_accum(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride,
-                              ctypes.byref(st))
+    _chk(lib().oracle_render_accum(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride,
+                                   ctypes.byref(st)))
     return acc, st.as_dict()
 
 
@@ -103,8 +110,8 @@ def render_range(desc: int, s_begin: int, s_end: int, nthreads: int = 1, tile_of
     w, h = film_size(desc)
     acc = np.zeros((h, w, 4), np.float32)
     st = oracle_stats()
-    lib().oracle_render_range(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride, s_begin,
-                              s_end, ctypes.byref(st))
+    _chk(lib().oracle_render_range(ctypes.c_void_p(desc), acc.ctypes.data, nthreads, tile_offset, tile_stride,
+                                   s_begin, s_end, ctypes.byref(st)))
     return acc, st.as_dict()
 
 

@@ -1066,8 +1066,21 @@ class Loader {
         if (sampler_.name != "halton") throw PtError(PT_ERR_UNSUPPORTED, "sampler \"" + sampler_.name + "\"");
         d.sampler.spp = sampler_.ps.int1("pixelsamples", 16);
         d.sampler.sample_pixel_center = sampler_.ps.bool1("samplepixelcenter", false) ? 1 : 0;
-        // Integrator (path.cpp:191-214)
-        if (integrator_.name != "path") throw PtError(PT_ERR_UNSUPPORTED, "integrator \"" + integrator_.name + "\"");
+        // Integrator (path.cpp:191-214, directlighting.cpp:86-118)
+        if (integrator_.name == "path") {
+            d.integrator.kind = PT_INTEGRATOR_PATH;
+        } else if (integrator_.name == "directlighting") {
+            d.integrator.kind = PT_INTEGRATOR_DIRECT;
+            const std::string st = integrator_.ps.string1("strategy", "all");
+            if (st == "one") d.integrator.direct_strategy = PT_DIRECT_ONE;
+            else {
+                if (st != "all")
+                    std::fprintf(stderr, "Warning: Strategy \"%s\" for direct lighting unknown. Using \"all\".\n",
+                                 st.c_str());
+                d.integrator.direct_strategy = PT_DIRECT_ALL;
+            }
+        } else
+            throw PtError(PT_ERR_UNSUPPORTED, "integrator \"" + integrator_.name + "\"");
         d.integrator.max_depth = integrator_.ps.int1("maxdepth", 5);
         d.integrator.rr_threshold = integrator_.ps.float1("rrthreshold", 1.f);
         std::string ls = integrator_.ps.string1("lightsamplestrategy", "uniform");

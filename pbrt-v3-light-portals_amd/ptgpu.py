@@ -117,6 +117,47 @@ class _desc_prefix(ctypes.Structure):
                 ("materials", ctypes.POINTER(pt_material))]
 
 
+class pt_transform(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_float * 16), ("minv", ctypes.c_float * 16)]
+
+
+class pt_camera_desc(ctypes.Structure):
+    _fields_ = [("camera_to_world", pt_transform), ("fov", ctypes.c_float), ("screen_window", ctypes.c_float * 4),
+                ("lens_radius", ctypes.c_float), ("focal_distance", ctypes.c_float),
+                ("shutter_open", ctypes.c_float), ("shutter_close", ctypes.c_float)]
+
+
+class pt_film_desc(ctypes.Structure):
+    _fields_ = [("xres", ctypes.c_int32), ("yres", ctypes.c_int32), ("crop", ctypes.c_float * 4),
+                ("filter", ctypes.c_int32), ("filter_radius", ctypes.c_float * 2), ("gaussian_alpha", ctypes.c_float),
+                ("scale", ctypes.c_float), ("max_sample_luminance", ctypes.c_float), ("diagonal", ctypes.c_float)]
+
+
+class pt_sampler_desc(ctypes.Structure):
+    _fields_ = [("spp", ctypes.c_int32), ("sample_pixel_center", ctypes.c_int32)]
+
+
+class pt_integrator_desc(ctypes.Structure):
+    _fields_ = [("max_depth", ctypes.c_int32), ("rr_threshold", ctypes.c_float), ("light_strategy", ctypes.c_int32),
+                ("has_pixel_bounds", ctypes.c_int32), ("pixel_bounds", ctypes.c_int32 * 4), ("kind", ctypes.c_int32),
+                ("direct_strategy", ctypes.c_int32)]
+
+
+class pt_scene_desc(ctypes.Structure):
+    """include/pt.h pt_scene_desc (read-only view of the loader's output)."""
+    _fields_ = _desc_prefix._fields_ + [
+        ("n_lights", ctypes.c_int32), ("lights", ctypes.c_void_p), ("n_portals", ctypes.c_int32),
+        ("portals", ctypes.c_void_p), ("bvh_max_prims", ctypes.c_int32), ("camera", pt_camera_desc),
+        ("film", pt_film_desc), ("sampler", pt_sampler_desc), ("integrator", pt_integrator_desc),
+        ("n_spheres", ctypes.c_int32), ("spheres", ctypes.c_void_p)]
+
+
+def integrator_desc(hs: "HostScene") -> pt_integrator_desc:
+    """A copy of the scene's pt_integrator_desc -- host only."""
+    d = ctypes.cast(ctypes.c_void_p(hs.desc), ctypes.POINTER(pt_scene_desc)).contents
+    return pt_integrator_desc.from_buffer_copy(d.integrator)
+
+
 class HostScene:
     """pbrtParseFile + pbrtWorldEnd (src/core/parser.cpp:1094, api.cpp:1702):
     the flattened world-space scene (pt_scene_desc) -- host only."""

@@ -54,3 +54,21 @@ def test_null_arguments_rejected():
     assert L.pt_render(None, None, None) == 1
     assert L.pt_scene_bvh(None, None, None, None, None) == 1
     assert L.pt_last_error()
+
+
+def test_ctypes_mirror_matches_c_layout():
+    """ptgpu's ctypes view of pt_scene_desc has the C layout (size and the
+    offsets the tests read)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "t.c")
+        open(src, "w").write('#include <stdio.h>\n#include <stddef.h>\n#include "pt.h"\nint main(void){printf("%zu %zu %zu %zu",'
+                             ' sizeof(pt_scene_desc), offsetof(pt_scene_desc, integrator), '
+                             'offsetof(pt_scene_desc, n_spheres), sizeof(pt_material));return 0;}\n')
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), src, "-o", exe])
+        got = [int(x) for x in subprocess.check_output([exe]).split()]
+    import ctypes
+    D = ptgpu.pt_scene_desc
+    assert got == [ctypes.sizeof(D), D.integrator.offset, D.n_spheres.offset, ctypes.sizeof(ptgpu.pt_material)]
