@@ -566,7 +566,11 @@ __device__ __forceinline__ S3 fr_conductor(float cosThetaI, S3 etat, S3 k) {
 // ----------------------------------------------------------------------------
 constexpr int kBxR = 1, kBxT = 2, kBxDiffuse = 4, kBxGlossy = 8, kBxSpecular = 16, kBxAll = 31;  // BxDFType
 constexpr int kBxNonSpecular = kBxAll & ~kBxSpecular;
-enum LobeKind { kLbLambert = 1, kLbMfRefl = 2, kLbMfTrans = 3, kLbFresnelSpec = 4, kLbSpecRefl = 5 };
+// kLbSpecRefl: SpecularReflection with FresnelNoOp (mirror); kLbSpecReflD / kLbSpecTrans:
+// SpecularReflection(FresnelDielectric) / SpecularTransmission, the smooth
+// dielectric when allowMultipleLobes is false (DirectLightingIntegrator).
+enum LobeKind { kLbLambert = 1, kLbMfRefl = 2, kLbMfTrans = 3, kLbFresnelSpec = 4, kLbSpecRefl = 5, kLbSpecReflD = 6,
+                kLbSpecTrans = 7 };
 
 // Scene features the shading code is compiled for (template argument kFt).
 // The host picks the smallest instantiation covering the scene (render.hip,
@@ -585,7 +589,7 @@ struct Ft {
     static constexpr bool spec = (kFt & kFtSpecular) != 0;
     static constexpr bool inf = (kFt & kFtInfinite) != 0;
     static constexpr bool sph = (kFt & kFtSphere) != 0;
-    static constexpr int max_lobes = micro ? 2 : 1;
+    static constexpr int max_lobes = (micro || spec) ? 2 : 1;
 };
 
 __device__ __forceinline__ int lobe_type(int k) {
@@ -594,6 +598,7 @@ __device__ __forceinline__ int lobe_type(int k) {
         case kLbMfRefl: return kBxR | kBxGlossy;
         case kLbMfTrans: return kBxT | kBxGlossy;
         case kLbFresnelSpec: return kBxR | kBxT | kBxSpecular;
+        case kLbSpecTrans: return kBxT | kBxSpecular;
         default: return kBxR | kBxSpecular;
     }
 }
@@ -743,6 +748,22 @@ __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, f
         *pdf = 1;
         return (s3(1.f) * clamp0(s3(m->kr[0], m->kr[1], m->kr[2]))) / fabsf(wi->z);
     }
+    if (k == kLbSpecReflD) {  // SpecularReflection::Sample_f (reflection.h:400-410), FresnelDielectric(1, eta)
+        *wi = refl_z(wo);
+        *pdf = 1;
+        return (s3(fr_dielectric(wi->z, 1.f, b.eta)) * clamp0(s3(m->kr[0], m->kr[1], m->kr[2]))) / fabsf(wi->z);
+    }
+    if (k == kLbSpecTrans) {  // SpecularTransmission::Sample_f (reflection.cpp:183-199), etaA = 1, etaB = eta
+        const bool entering = wo.z > 0;
+        const float etaI = entering ? 1.f : b.eta;
+        const float etaT = entering ? b.eta : 1.f;
+        const V3 n = dot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1);  // Faceforward(n, wo)
+        if (!refract(wo, n, etaI / etaT, wi)) return s3(0.f);
+        *pdf = 1;
+        S3 ft = clamp0(s3(m->kt[0], m->kt[1], m->kt[2])) * (s3(1.f) - s3(fr_dielectric(wi->z, 1.f, b.eta)));
+        ft = ft * ((etaI * etaI) / (etaT * etaT));  // TransportMode::Radiance
+        return ft / fabsf(wi->z);
+    }
     // FresnelSpecular::Sample_f (reflection.cpp:520-554), etaA = 1, etaB = eta
     const float F = fr_dielectric(wo.z, 1.f, b.eta);
     if (u0 < F) {
@@ -771,7 +792,8 @@ __device__ __forceinline__ void add_lobe(Bsdf* b, int k) {
 // Material::ComputeScatteringFunctions(..., Radiance, allowMultipleLobes = true)
 // + BSDF ctor (reflection.h:167-172).  wvl0: the camera's hero wavelength.
 template <int kFt = kFtAll>
-__device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, float wvl0, Bsdf* b) {
+__device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& si, float wvl0, Bsdf* b,
+                                          bool multi = true) {
     b->ns = si.sn;
     b->ng = si.n;
     b->ss = normalize(si.sdpdu);
@@ -803,7 +825,11 @@ __device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& s
         const bool hasT = !is_black(clamp0(s3(m->kt[0], m->kt[1], m->kt[2])));
         if (!hasR && !hasT) return;
         if (Ft<kFt>::spec && (m->specular || !Ft<kFt>::micro)) {
-            add_lobe(b, kLbFresnelSpec);
+            if (multi) add_lobe(b, kLbFresnelSpec);
+            else {  // glass.cpp:66-83 with isSpecular
+                if (hasR) add_lobe(b, kLbSpecReflD);
+                if (hasT) add_lobe(b, kLbSpecTrans);
+            }
         } else if (Ft<kFt>::micro) {
             if (hasR) add_lobe(b, kLbMfRefl);
             if (hasT) add_lobe(b, kLbMfTrans);

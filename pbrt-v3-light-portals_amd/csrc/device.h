@@ -38,6 +38,7 @@ struct DevSphere {
 
 struct DevLight {
     int kind;
+    int n_samples;
     S3 L;
     int two_sided;
     int shape;
@@ -95,9 +96,14 @@ struct DevScene {
     M4 r2c;
     M4 c2w;
     float lens_radius, focal_distance;
-    // integrator (integrators/path.cpp)
+    // integrator (integrators/path.cpp, directlighting.cpp)
     int max_depth;
     float rr_threshold;
+    int integrator;         // pt_integrator_kind
+    int dl_strategy;        // pt_direct_strategy
+    int dl_arrays;          // 2D sample arrays requested (0 unless "all")
+    int dl_frames;          // recursion stack frames allocated per sample
+    int wvl_dim;            // Halton dimension of CameraSample::wvl (5, or arrayEndDim with arrays)
 };
 
 // Per-path SoA state for one batch of nslots camera samples.
@@ -116,7 +122,39 @@ struct DevPaths {
     float* rayB;        // 6n NEE ray B o,d
     int* hitB;          // n
     float* nee;         // kNee * n payload
+    // DirectLightingIntegrator only (null otherwise): see kDl* below
+    int* dli;           // kDlInts * n
+    float* dlf;         // kDlFloats * n
+    float* dlframe;     // kDlFrame * frames * n: the specular recursion stack
 };
+
+// DirectLightingIntegrator per-sample state (kernels.hip shade_dl).
+// Integer fields (dli[k * n + slot]):
+constexpr int kDlD = 0;      // current recursion depth (frame index)
+constexpr int kDlJ = 1;      // UniformSampleAllLights: current light
+constexpr int kDlK = 2;      //   current array entry
+constexpr int kDlN = 3;      //   entries in the current light's arrays
+constexpr int kDlAoff = 4;   // Sampler::array2DOffset
+constexpr int kDlAi = 5;     // index of the current uLight array (uScattering = +1)
+constexpr int kDlMode = 6;   // kind of the pending EstimateDirect (kDlMode*)
+constexpr int kDlS = 7;      // pixel sample number (sample-array indices s*n .. s*n+n-1)
+constexpr int kDlPix = 8;    // the pixel's Halton offset (GetIndexForSample(0))
+constexpr int kDlInts = 9;
+constexpr int kDlModeArray = 0, kDlModeSingle = 1, kDlModeOne = 2;
+// Float fields (dlf[k * n + slot]):
+constexpr int kDlLnee = 0;   // 3: UniformSampleAllLights' running sum over lights
+constexpr int kDlLd = 3;     // 3: current light's sum over array entries
+constexpr int kDlLpdf = 6;   // "one": light selection pdf
+constexpr int kDlFloats = 7;
+// Frame f fields (dlframe[(f * kDlFrame + k) * n + slot]):
+constexpr int kFrL = 0;      // 3: the vertex's L so far
+constexpr int kFrRay = 3;    // 6: the ray that found the vertex (to rebuild its BSDF)
+constexpr int kFrPrim = 9;   // hit primitive (int bits)
+constexpr int kFrFac = 10;   // 3: f of the pending specular child
+constexpr int kFrCos = 13;   // |wi . ns|
+constexpr int kFrPdf = 14;   // pdf
+constexpr int kFrPhase = 15; // 0: reflection child pending (transmission next), 1: transmission child
+constexpr int kDlFrame = 16;
 
 // st bits
 constexpr uint32_t kStDimMask = 0xffffu;

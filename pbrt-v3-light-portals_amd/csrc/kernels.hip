@@ -561,7 +561,15 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
         ps.L[slot] = 0.f; ps.L[N + slot] = 0.f; ps.L[2 * N + slot] = 0.f;
         ps.beta[slot] = 1.f; ps.beta[N + slot] = 1.f; ps.beta[2 * N + slot] = 1.f;
         ps.eta[slot] = 1.f;
-        ps.st[slot] = 6u | kStCont;  // dims 0-5 consumed (pFilm, time, pLens, wvl)
+        // dims 0-4 (pFilm, time, pLens) and the wvl dimension consumed; with sample
+        // arrays Get1D jumps over [5, arrayEndDim) for wvl (sampler.cpp:180-184)
+        ps.st[slot] = (uint32_t)(sc.wvl_dim + 1) | kStCont;
+        if (ps.dli) {
+            ps.dli[kDlD * N + slot] = 0;
+            ps.dli[kDlAoff * N + slot] = 0;
+            ps.dli[kDlS * N + slot] = s0 + (int)sl;
+            ps.dli[kDlPix * N + slot] = (int)off;
+        }
         store_ray6(ps.ray, N, slot, r);
         rq[slot] = slot << 2 | kRayCont;
         pq[slot] = slot;
@@ -606,8 +614,10 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 
 // Finish the NEE of the previous vertex: Ld from the traced rays, then
 // L += beta * Ld / lightPdf (integrator.cpp:121, path.cpp:122-127).
+// EstimateDirect's value from its traced rays (integrator.cpp:124-258,
+// portal_arealight.cpp:29-239): the Ld of the previous vertex's NEE.
 template <int kFt>
-__device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, S3* L) {
+__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
     const uint32_t fl = __float_as_uint(nee[kNeeFlags * N + slot]);
@@ -644,6 +654,13 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
             }
         }
     }
+    return Ld;
+}
+template <int kFt>
+__device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, S3* L) {
+    const uint32_t N = (uint32_t)ps.n;
+    const float* nee = ps.nee;
+    const S3 Ld = nee_value<kFt>(sc, ps, slot);
     const S3 bv = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
     *L = *L + bv * (Ld / nee[kNeeLpdf * N + slot]);
 }
@@ -858,7 +875,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
                 const float wvl0 = Ft<kFt>::spec && sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
-                                       ? (float)400 + (float)300 * halton_dim(sc, dm.idx, 5) : 550.f;
+                                       ? (float)400 + (float)300 * halton_dim(sc, dm.idx, sc.wvl_dim) : 550.f;
                 make_bsdf<kFt>(&sc.mats[mat], si, wvl0, &bsdf);
                 if (bsdf_num<kFt>(bsdf, kBxNonSpecular) > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
@@ -953,6 +970,285 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         if (i < n) {
             slot = pq[i];
             shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
+        }
+        const uint32_t pos = wave_reserve(rq_out_count, nrays);
+        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
+        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
+        if (keep) pq_out[ppos] = slot;
+    }
+    if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
+}
+
+// ----------------------------------------------------------------------------
+// DirectLightingIntegrator::Li (directlighting.cpp:58-84) as a resumable
+// per-sample state machine.  The reference recurses depth first through
+// SpecularReflect / SpecularTransmit (integrator.cpp:639-770) and consumes
+// sampler dimensions in that order, and it sums each vertex's radiance before
+// its parent scales it (f * Li * |cos| / pdf), so the device keeps an explicit
+// stack of frames (DevPaths::dlframe) and resumes a parent when its child's
+// subtree returns.  Each EstimateDirect of UniformSampleAllLights (one per
+// sample-array entry) or UniformSampleOneLight is one wavefront step: its rays
+// are traced, then nee_value() gives its Ld and the sum continues in the
+// reference's order.
+// ----------------------------------------------------------------------------
+enum DlStep { kDlHit, kDlLights, kDlOne, kDlAcc, kDlSpecR, kDlSpecT, kDlReturn, kDlDone };
+
+template <int kFt>
+__device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
+                                         uint32_t* nrays, bool* keep, bool* overflow) {
+    const uint32_t N = (uint32_t)ps.n;
+    int* const I = ps.dli;
+    float* const Fl = ps.dlf;
+    float* const FR = ps.dlframe;
+    auto fr = [&](int d, int k) -> float& { return FR[(size_t)(d * kDlFrame + k) * N + slot]; };
+    auto fr3 = [&](int d, int k) { return s3(fr(d, k), fr(d, k + 1), fr(d, k + 2)); };
+    auto set3 = [&](int d, int k, S3 v) { fr(d, k) = v.c[0]; fr(d, k + 1) = v.c[1]; fr(d, k + 2) = v.c[2]; };
+    auto fl3 = [&](int k) { return s3(Fl[k * N + slot], Fl[(k + 1) * N + slot], Fl[(k + 2) * N + slot]); };
+    auto setf3 = [&](int k, S3 v) { Fl[k * N + slot] = v.c[0]; Fl[(k + 1) * N + slot] = v.c[1]; Fl[(k + 2) * N + slot] = v.c[2]; };
+
+    uint32_t st = ps.st[slot];
+    *nrays = 0;
+    int d = I[kDlD * N + slot];
+    Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+    int step;
+    S3 e = s3(0.f), Lc = s3(0.f);
+    if (st & kStNee) {
+        e = nee_value<kFt>(sc, ps, slot);
+        st &= ~kStNee;
+        step = kDlAcc;
+    } else {
+        st &= ~kStCont;
+        step = kDlHit;
+    }
+    // the current frame's vertex (rebuilt from its stored ray when resuming)
+    bool haveV = false;
+    SurfHit si{};
+    Bsdf bsdf{};
+    auto vertex = [&]() {
+        if (haveV) return;
+        const Ray r{v3(fr(d, kFrRay), fr(d, kFrRay + 1), fr(d, kFrRay + 2)),
+                    v3(fr(d, kFrRay + 3), fr(d, kFrRay + 4), fr(d, kFrRay + 5)), kInf};
+        const int prim = __float_as_int(fr(d, kFrPrim));
+        surface_at<Ft<kFt>::sph>(sc, prim, r, &si);
+        int mat, light;
+        prim_info<Ft<kFt>::sph>(sc, prim, &mat, &light);
+        const float wvl0 = Ft<kFt>::spec && sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
+                               ? (float)400 + (float)300 * halton_dim(sc, dm.idx, sc.wvl_dim) : 550.f;
+        make_bsdf<kFt>(&sc.mats[mat], si, wvl0, &bsdf, false);
+        haveV = true;
+    };
+    // one EstimateDirect: emits its rays, or yields Ld = 0 at once
+    auto estimate = [&](int j, float uL0, float uL1, float uS0, float uS1) -> bool {
+        vertex();
+        if (sc.lights[j].kind == PT_LIGHT_PORTAL_AREA) {
+            if (portal_nee<kFt>(sc, ps, slot, j, si, bsdf, uS0, uS1)) {
+                rays[(*nrays)++] = slot << 2 | kRayA;
+                return true;
+            }
+            return false;
+        }
+        const uint32_t f = mis_nee<kFt>(sc, ps, slot, j, si, bsdf, uL0, uL1, uS0, uS1);
+        if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
+        if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
+        return (f & (kNfA | kNfB)) != 0;
+    };
+    // Sampler::Get2DArray entry k of array ai: GetIndexForSample(s * n + k) (sampler.cpp:149-160)
+    auto array_u = [&](int ai, int k, int n, float* u0, float* u1) {
+        const uint32_t idx = (uint32_t)I[kDlPix * N + slot] +
+                             ((uint32_t)I[kDlS * N + slot] * (uint32_t)n + (uint32_t)k) * sc.hal_stride;
+        *u0 = halton_dim(sc, idx, 5 + 2 * ai);
+        *u1 = halton_dim(sc, idx, 5 + 2 * ai + 1);
+    };
+    auto spawn_child = [&](S3 f, V3 wi, float pdf, int phase) {
+        set3(d, kFrFac, f);
+        fr(d, kFrCos) = absdot(wi, si.sn);
+        fr(d, kFrPdf) = pdf;
+        fr(d, kFrPhase) = __int_as_float(phase);
+        const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};  // SpawnRay
+        store_ray6(ps.ray, N, slot, r);
+        ++d;
+        haveV = false;
+        st |= kStCont;
+        rays[(*nrays)++] = slot << 2 | kRayCont;
+    };
+    bool emitted = false;
+    while (!emitted && step != kDlDone) {
+        switch (step) {
+            case kDlHit: {
+                const Ray ray = load_ray6(ps.ray, N, slot, kInf);
+                const int hp = ps.hit[slot];
+                SurfHit h;
+                const bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &h);
+                if (!found) {  // Light::Le of every light: only infinite lights emit
+                    S3 Lm = s3(0.f);
+                    if (Ft<kFt>::inf)
+                        for (int li = 0; li < sc.n_lights; ++li)
+                            if (sc.lights[li].kind == PT_LIGHT_INFINITE) Lm = Lm + inf_Le(sc.lights[li], ray.d);
+                    Lc = Lm;
+                    step = kDlReturn;
+                    break;
+                }
+                int mat, light;
+                prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
+                if (sc.mats[mat].kind == PT_MAT_NONE) {  // Li(isect.SpawnRay(ray.d), depth)
+                    const Ray r{offset_ray_origin(h.p, h.perr, h.n, ray.d), ray.d, kInf};
+                    store_ray6(ps.ray, N, slot, r);
+                    st |= kStCont;
+                    rays[(*nrays)++] = slot << 2 | kRayCont;
+                    emitted = true;
+                    break;
+                }
+                for (int c = 0; c < 3; ++c) { fr(d, kFrRay + c) = ray.o[c]; fr(d, kFrRay + 3 + c) = ray.d[c]; }
+                fr(d, kFrPrim) = __int_as_float(hp);
+                haveV = false;
+                vertex();
+                const S3 Le = light >= 0 ? area_L(sc.lights[light], si.n, si.wo) : s3(0.f);  // isect.Le(wo)
+                set3(d, kFrL, s3(0.f) + Le);
+                if (sc.n_lights > 0) {
+                    if (sc.dl_strategy == PT_DIRECT_ALL) {
+                        setf3(kDlLnee, s3(0.f));
+                        I[kDlJ * N + slot] = 0;
+                        step = kDlLights;
+                    } else
+                        step = kDlOne;
+                } else
+                    step = kDlSpecR;
+                break;
+            }
+            case kDlLights: {  // UniformSampleAllLights (integrator.cpp:69-98), light j
+                const int j = I[kDlJ * N + slot];
+                if (j == sc.n_lights) {
+                    set3(d, kFrL, fr3(d, kFrL) + fl3(kDlLnee));
+                    step = kDlSpecR;
+                    break;
+                }
+                const int n = sc.lights[j].n_samples;
+                int aoff = I[kDlAoff * N + slot];
+                const int a1 = aoff < sc.dl_arrays ? aoff++ : -1;
+                const int a2 = aoff < sc.dl_arrays ? aoff++ : -1;
+                I[kDlAoff * N + slot] = aoff;
+                float uL0, uL1, uS0, uS1;
+                if (a1 < 0 || a2 < 0) {
+                    I[kDlMode * N + slot] = kDlModeSingle;
+                    uL0 = dm.get1(); uL1 = dm.get1();
+                    uS0 = dm.get1(); uS1 = dm.get1();
+                } else {
+                    I[kDlMode * N + slot] = kDlModeArray;
+                    I[kDlK * N + slot] = 0;
+                    I[kDlN * N + slot] = n;
+                    I[kDlAi * N + slot] = a1;
+                    setf3(kDlLd, s3(0.f));
+                    array_u(a1, 0, n, &uL0, &uL1);
+                    array_u(a2, 0, n, &uS0, &uS1);
+                }
+                if (estimate(j, uL0, uL1, uS0, uS1)) { st |= kStNee; emitted = true; }
+                else { e = s3(0.f); step = kDlAcc; }
+                break;
+            }
+            case kDlOne: {  // UniformSampleOneLight without a distribution (integrator.cpp:100-122)
+                const int nl = sc.n_lights;
+                const int ln = min((int)(dm.get1() * nl), nl - 1);
+                Fl[kDlLpdf * N + slot] = (float)1 / nl;
+                const float uL0 = dm.get1(), uL1 = dm.get1();
+                const float uS0 = dm.get1(), uS1 = dm.get1();
+                I[kDlMode * N + slot] = kDlModeOne;
+                if (estimate(ln, uL0, uL1, uS0, uS1)) { st |= kStNee; emitted = true; }
+                else { e = s3(0.f); step = kDlAcc; }
+                break;
+            }
+            case kDlAcc: {
+                const int mode = I[kDlMode * N + slot];
+                if (mode == kDlModeArray) {
+                    const S3 Ld = fl3(kDlLd) + e;
+                    const int k = I[kDlK * N + slot] + 1, n = I[kDlN * N + slot];
+                    if (k < n) {
+                        setf3(kDlLd, Ld);
+                        I[kDlK * N + slot] = k;
+                        const int ai = I[kDlAi * N + slot];
+                        float uL0, uL1, uS0, uS1;
+                        array_u(ai, k, n, &uL0, &uL1);
+                        array_u(ai + 1, k, n, &uS0, &uS1);
+                        if (estimate(I[kDlJ * N + slot], uL0, uL1, uS0, uS1)) { st |= kStNee; emitted = true; }
+                        else { e = s3(0.f); step = kDlAcc; }
+                    } else {
+                        setf3(kDlLnee, fl3(kDlLnee) + Ld / (float)n);
+                        I[kDlJ * N + slot] += 1;
+                        step = kDlLights;
+                    }
+                } else if (mode == kDlModeSingle) {
+                    setf3(kDlLnee, fl3(kDlLnee) + e);
+                    I[kDlJ * N + slot] += 1;
+                    step = kDlLights;
+                } else {
+                    set3(d, kFrL, fr3(d, kFrL) + e / Fl[kDlLpdf * N + slot]);
+                    step = kDlSpecR;
+                }
+                break;
+            }
+            case kDlSpecR:
+            case kDlSpecT: {  // SpecularReflect / SpecularTransmit (integrator.cpp:639-770)
+                if (step == kDlSpecR && !(d + 1 < sc.max_depth)) {
+                    Lc = fr3(d, kFrL);
+                    step = kDlReturn;
+                    break;
+                }
+                const float u0 = dm.get1(), u1 = dm.get1();
+                vertex();
+                V3 wi = v3(0, 0, 0);
+                float pdf = 0;
+                int sampled = 0;
+                const int type = (step == kDlSpecR ? kBxR : kBxT) | kBxSpecular;
+                const S3 f = bsdf_sample<kFt>(bsdf, si.wo, &wi, u0, u1, &pdf, type, &sampled);
+                if (pdf > 0.f && !is_black(f) && absdot(wi, si.sn) != 0.f) {
+                    spawn_child(f, wi, pdf, step == kDlSpecR ? 0 : 1);
+                    emitted = true;
+                } else if (step == kDlSpecR) {
+                    step = kDlSpecT;
+                } else {
+                    Lc = fr3(d, kFrL);
+                    step = kDlReturn;
+                }
+                break;
+            }
+            case kDlReturn: {
+                if (d == 0) {
+                    store_s3(ps.L, N, slot, Lc);
+                    step = kDlDone;
+                    break;
+                }
+                --d;
+                haveV = false;
+                set3(d, kFrL, fr3(d, kFrL) + ((fr3(d, kFrFac) * Lc) * fr(d, kFrCos)) / fr(d, kFrPdf));
+                if (__float_as_int(fr(d, kFrPhase)) == 0) step = kDlSpecT;
+                else { Lc = fr3(d, kFrL); step = kDlReturn; }
+                break;
+            }
+            default: step = kDlDone; break;
+        }
+    }
+    I[kDlD * N + slot] = d;
+    if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
+    st = (st & ~kStDimMask) | ((uint32_t)dm.dim & kStDimMask);
+    ps.st[slot] = st;
+    *keep = (st & (kStCont | kStNee)) != 0;
+}
+
+template <int kFt>
+__global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
+                                                          const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                                          uint32_t* rq_out_count, uint32_t* pq_out,
+                                                          uint32_t* pq_out_count, DevStats* stats) {
+    const uint32_t n = *pq_count;
+    bool overflow = false;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t rays[3];
+        uint32_t nrays = 0;
+        bool keep = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = pq[i];
+            shade_dl<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
         }
         const uint32_t pos = wave_reserve(rq_out_count, nrays);
         for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
@@ -1127,7 +1423,7 @@ __global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float
     SurfHit si{};
     si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
     Bsdf b;
-    make_bsdf(&sc.mats[mat], si, 550.f, &b);
+    make_bsdf(&sc.mats[mat], si, 550.f, &b, sc.integrator != PT_INTEGRATOR_DIRECT);
     const V3 wo = v3(a[0], a[1], a[2]), wi = v3(a[3], a[4], a[5]);
     float* o = out + 8 * i;
     S3 f = s3(0.f);

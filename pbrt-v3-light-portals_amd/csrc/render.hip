@@ -148,8 +148,17 @@ struct Work {
     DBuf<float> L, beta, eta, ray, rayA, rayB, nee;
     DBuf<int> hit, hitA, hitB, spill;
     DBuf<DevStats> stats;
+    DBuf<int> dli;                 // DirectLighting state (kDl*)
+    DBuf<float> dlf, dlframe;
     size_t cap = 0;
-    void ensure(size_t n, size_t spill_threads) {
+    int dl_frames = 0;             // > 0: DirectLighting buffers with this many frames per slot
+    void ensure(size_t n, size_t spill_threads, int frames) {
+        if (frames > 0 && (n > cap || frames != dl_frames)) {
+            dli.alloc((size_t)kDlInts * n);
+            dlf.alloc((size_t)kDlFloats * n);
+            dlframe.alloc((size_t)kDlFrame * (size_t)frames * n);
+            dl_frames = frames;
+        }
         if (n > cap) {
             hidx.alloc(n); st.alloc(n); rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
             pfilm.alloc(n); L.alloc(3 * n); beta.alloc(3 * n); eta.alloc(n); ray.alloc(6 * n); rayA.alloc(7 * n);
@@ -166,6 +175,9 @@ struct Work {
         p.hidx = hidx.p; p.pfilm = pfilm.p; p.L = L.p; p.beta = beta.p; p.eta = eta.p; p.st = st.p;
         p.ray = ray.p; p.hit = hit.p; p.rayA = rayA.p; p.hitA = hitA.p; p.rayB = rayB.p; p.hitB = hitB.p;
         p.nee = nee.p;
+        p.dli = dl_frames > 0 ? dli.p : nullptr;
+        p.dlf = dl_frames > 0 ? dlf.p : nullptr;
+        p.dlframe = dl_frames > 0 ? dlframe.p : nullptr;
         return p;
     }
 };
@@ -195,6 +207,7 @@ struct pt_scene {
     int device = 0;
     int num_cus = 256;
     size_t target_slots = (size_t)8 << 20;
+    int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
@@ -216,6 +229,7 @@ static int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 // same image: the extra code is simply unreachable).
 static int scene_features(const pt_scene_desc* d) {
     int f = 0;
+    if (!d || (d->n_materials > 0 && !d->materials) || (d->n_lights > 0 && !d->lights)) return kFtAll;
     for (int i = 0; i < d->n_materials; ++i) {
         const pt_material& m = d->materials[i];
         if (m.kind == PT_MAT_METAL || m.kind == PT_MAT_PLASTIC) f |= kFtMicro;
@@ -494,6 +508,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         dl.strategy = l.strategy;
         dl.first_portal = l.first_portal;
         dl.n_portals = l.n_portals;
+        dl.n_samples = std::max(1, l.n_samples);
         if (l.kind == PT_LIGHT_INFINITE) init_infinite(l, s->host_nodes, &dl);
         else if (l.kind == PT_LIGHT_DIFFUSE_AREA) dl.area = area[l.shape];
         else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) dl.area = spheres[l.shape].area;
@@ -618,7 +633,10 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     s->hpc.scale0 = (uint32_t)scales[0];
     s->hpc.mi0 = (uint32_t)mult_inverse(scales[1], scales[0]);
     s->hpc.mi1 = (uint32_t)mult_inverse(scales[0], scales[1]);
-    int max_dim = std::min(1000, 6 + 8 * (d->integrator.max_depth + 1));
+    // DirectLighting: the sample arrays occupy [5, 5 + 2 * arrays) and the
+    // recursion's dimensions depend on the scene, so keep every prime.
+    const bool direct = d->integrator.kind == PT_INTEGRATOR_DIRECT;
+    int max_dim = direct ? 1000 : std::min(1000, 6 + 8 * (d->integrator.max_depth + 1));
     std::vector<DivMagic> divs((size_t)max_dim);
     std::vector<float> c0((size_t)max_dim);
     for (int i = 0; i < max_dim; ++i) {
@@ -678,6 +696,22 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     ds.focal_distance = cam.focal_distance;
     ds.max_depth = d->integrator.max_depth;
     ds.rr_threshold = d->integrator.rr_threshold;
+    ds.integrator = d->integrator.kind;
+    ds.dl_strategy = d->integrator.direct_strategy;
+    ds.dl_arrays = 0;
+    ds.dl_frames = 0;
+    if (direct) {
+        // DirectLightingIntegrator::Preprocess (directlighting.cpp:43-56): "all"
+        // requests two 2D arrays of nSamples per light per depth
+        if (ds.dl_strategy == PT_DIRECT_ALL && d->n_lights > 0) ds.dl_arrays = 2 * d->n_lights * ds.max_depth;
+        if (5 + 2 * ds.dl_arrays >= 1000)
+            throw PtError(PT_ERR_UNSUPPORTED, "DirectLighting sample arrays exceed the Halton dimension table");
+        // recursion frames: specular lobes are the only way below depth 0
+        ds.dl_frames = (s->features & kFtSpecular) ? std::max(1, ds.max_depth) : 1;
+        s->dl_max_samples = 1;
+        for (int i = 0; i < d->n_lights; ++i) s->dl_max_samples = std::max(s->dl_max_samples, d->lights[i].n_samples);
+    }
+    ds.wvl_dim = ds.dl_arrays > 0 ? 5 + 2 * ds.dl_arrays : 5;
 }
 
 // Pixels of tiles t with t % stride == offset, tile order then scan order
@@ -729,6 +763,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     if (s_begin < 0 || s_end < s_begin) throw PtError(PT_ERR_INVALID_ARG, "bad sample range");
     if ((uint64_t)s->dev.hal_stride * (uint64_t)s_end > 0xffffffffull)
         throw PtError(PT_ERR_UNSUPPORTED, "Halton sample index exceeds 32 bits");
+    if (s->dev.dl_arrays > 0 &&  // sample-array entries use indices up to s_end * nSamples
+        (uint64_t)s->dev.hal_stride * (uint64_t)s_end * (uint64_t)s->dl_max_samples > 0xffffffffull)
+        throw PtError(PT_ERR_UNSUPPORTED, "Halton sample-array index exceeds 32 bits");
     const Frame& fr = s->fr;
     std::vector<int2> pix;
     std::vector<TileSpan> tiles;
@@ -784,7 +821,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     const int maxBlocksTrace = s->num_cus * 16;
     const int maxBlocksShade = s->num_cus * 8;
     Work& w = s->work;
-    w.ensure(max_slots, (size_t)std::max(maxBlocksTrace, s->num_cus * s->trace_bpc) * kTraceBlock);
+    const bool direct = s->dev.integrator == PT_INTEGRATOR_DIRECT;
+    w.ensure(max_slots, (size_t)std::max(maxBlocksTrace, s->num_cus * s->trace_bpc) * kTraceBlock,
+             direct ? s->dev.dl_frames : 0);
     HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
     DevPaths ps = w.paths((int)max_slots);
     hipEvent_t ev0, ev1;
@@ -847,7 +886,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     rr.launches++;
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
-                const ShadeKernel kshade = shade_kernel(s->shade_variant, s->features);
+                const ShadeKernel kshade = direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
                 hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out,
                                    counts + 2, pq_out, counts + 3, w.stats.p);
                 HIPCHK(hipGetLastError());
@@ -1028,6 +1067,8 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, s->device));
         s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        s->features = scene_features(desc);
+        if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
         build_scene(s.get(), desc);
         const int sbound = bvh_stack_bound(s->host_nodes);
         s->trace_spill = sbound > kStackLds;
@@ -1044,8 +1085,6 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                  ? scene_bytes : 0;
         const char* v = std::getenv("PT_SHADE_VARIANT");
         if (v) s->shade_variant = std::atoi(v);
-        s->features = scene_features(desc);
-        if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
         s->has_spheres = (s->features & kFtSphere) != 0;
         if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
         if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
