@@ -30,6 +30,13 @@ sys.path.insert(0, PKG)
 
 METRIC = "Msamples/sec + Mrays/sec, 1920x1080 path integrator @256spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# BASELINE.json configs this bench can run: scene file, workload label
+CONFIGS = {
+    "c2": ("portal_cornell.pbrt", "portal Cornell (config 2)", "path maxdepth 5",
+           "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)"),
+    "c4": ("portal_room.pbrt", "portal room (config 4)", "path maxdepth 8",
+           "synthetic (scenes/portal_room.pbrt from scripts/make_portal_room.py: room + 4 portals + sky; Halton)"),
+}
 
 
 def parse():
@@ -37,7 +44,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default=os.path.join(REPO, "scenes", "portal_cornell.pbrt"))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="c2: the headline workload (default); c4: portal room (BASELINE configs[3])")
+    ap.add_argument("--scene", default="", help="override the config's scene file")
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per rank (0 = scene)")
     ap.add_argument("--res", default="", help="override WxH")
     ap.add_argument("--strategy", default="", help="override portal strategy")
@@ -50,7 +59,7 @@ def parse():
 
 def scene_text(args) -> str:
     import re
-    txt = open(args.scene).read()
+    txt = open(args.scene or os.path.join(REPO, "scenes", CONFIGS[args.config][0])).read()
     if args.res:
         w, h = (int(v) for v in args.res.lower().split("x"))
         txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [%d]' % w, txt)
@@ -164,8 +173,9 @@ def main():
         total_samples, total_rays = float(agg["samples"]), float(agg["closest_rays"] + agg["shadow_rays"])
 
     if rank == 0:
-        workload = (f"portal Cornell (config 2) {w}x{h} @{spp}spp{'/rank' if args.shard == 'samples' else ''}, "
-                    f"path maxdepth 5, {args.shard}-sharded")
+        cname, cdepth, cdata = CONFIGS[args.config][1:]
+        workload = (f"{cname} {w}x{h} @{spp}spp{'/rank' if args.shard == 'samples' else ''}, "
+                    f"{cdepth}, {args.shard}-sharded")
         traffic, traffic_src = pmc_traffic(workload)
         alg_bytes = 32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]
         achieved = alg_bytes / (agg["trace_ms"] * 1e-3) / 1e9 if agg["trace_ms"] > 0 else 0.0
@@ -181,7 +191,7 @@ def main():
             "scaling": "weak" if args.shard == "samples" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)",
+            "data": cdata,
             "config": {"workload": workload, "resolution": [w, h],
                        "frame_spp": shardmod.frame_samples(spp, world, args.shard),
                        "parallelism": f"{args.shard} x{world}"},

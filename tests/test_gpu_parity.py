@@ -459,3 +459,18 @@ def test_directlighting_single_lobe_glass_bsdf_bit_exact(tmp_path):
     got = sc.debug_bsdf(mat, rec)
     ref = pyoracle.bsdf_batch(hs.desc, mat, rec)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("strategy", ["portal", "light", "projection"])
+def test_portal_room_matches_oracle(tmp_path, strategy):
+    """Config 4 (four portals on one emitter + an infinite light, maxdepth 8)
+    at a reduced film: device == oracle bit for bit."""
+    from conftest import scene_variant
+    hs, sc = _scene(scene_variant(tmp_path, name="portal_room.pbrt", res=(96, 54), spp=16, strategy=strategy))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"room/{strategy}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k

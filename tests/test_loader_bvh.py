@@ -11,6 +11,8 @@ import ptgpu
 import pyoracle
 from conftest import SCENES, furnace_scene
 
+REPO = os.path.dirname(SCENES)
+
 
 class Desc(ctypes.Structure):
     """Prefix of pt_scene_desc (include/pt.h) for inspection."""
@@ -123,3 +125,18 @@ def test_commas_in_numbers_are_tolerated(tmp_path):
     p.write_text(txt)
     hs = ptgpu.HostScene(str(p))
     assert _desc(hs).n_planes == 1
+
+
+def test_portal_room_scene(tmp_path):
+    """Config 4 scene (scripts/make_portal_room.py): four portals on one
+    PortalArealight, an infinite light, the committed file is what the
+    generator writes."""
+    import subprocess
+    import sys
+    out = tmp_path / "room.pbrt"
+    subprocess.check_call([sys.executable, os.path.join(REPO, "scripts", "make_portal_room.py"), str(out)])
+    assert out.read_text() == open(os.path.join(REPO, "scenes", "portal_room.pbrt")).read()
+    hs = ptgpu.HostScene(str(out))
+    d = ctypes.cast(ctypes.c_void_p(hs.desc), ctypes.POINTER(ptgpu.pt_scene_desc)).contents
+    assert (d.n_lights, d.n_portals, d.n_planes) == (2, 4, 1)
+    assert (d.film.xres, d.film.yres, d.sampler.spp, d.integrator.max_depth) == (3840, 2160, 1024, 8)
