@@ -34,6 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CONFIGS = {
     "c2": ("portal_cornell.pbrt", "portal Cornell (config 2)", "path maxdepth 5",
            "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)"),
+    "c3": ("cornell_dielectric.pbrt", "cornell dielectric (config 3)", "path maxdepth 5",
+           "reference scenes/cornell_dielectric.pbrt (spectral params reduced to RGB) with Integrator path, 1024 spp"),
     "c4": ("portal_room.pbrt", "portal room (config 4)", "path maxdepth 8",
            "synthetic (scenes/portal_room.pbrt from scripts/make_portal_room.py: room + 4 portals + sky; Halton)"),
 }
@@ -45,7 +47,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
-                    help="c2: the headline workload (default); c4: portal room (BASELINE configs[3])")
+                    help="c2: the headline workload (default); c3: cornell_dielectric (BASELINE configs[2]); "
+                         "c4: portal room (BASELINE configs[3])")
     ap.add_argument("--scene", default="", help="override the config's scene file")
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per rank (0 = scene)")
     ap.add_argument("--res", default="", help="override WxH")

@@ -351,6 +351,13 @@ pt_status pt_write_pfm(const char* path, const float* rgb, int32_t width, int32_
 /* The shared host/device sinf/cosf port used by ConcentricSampleDisk,
  * evaluated on the host (compare with the platform libm). */
 pt_status pt_debug_libm_trig(int n, const float* x, float* sin_out, float* cos_out);
+/* Spectral parameter reduction of the loader (RGBSpectrum build), on the host:
+ * kind 0: vals = n (lambda, value) pairs -> RGBSpectrum::FromSampled
+ *         (spectrum.h, paramset.cpp:152-169), out = rgb[3];
+ * kind 1: vals = (T, scale) -> blackbody parameter (paramset.cpp:134-150), out = rgb[3];
+ * kind 2: vals = xyz[3] -> FromXYZ (spectrum.h:58-62), out = rgb[3];
+ * kind 3: vals = n (lambda, T) pairs -> Blackbody() radiance (spectrum.cpp:939-955), out = n values. */
+pt_status pt_debug_spectrum(int kind, int n, const float* vals, float* out);
 /* HaltonSampler::SampleDimension(idx[i], dims[i]) on the device. */
 pt_status pt_debug_halton(pt_scene* scene, int n, const uint32_t* idx, const int32_t* dims, float* out);
 /* HaltonSampler per-pixel offsets for (x, y) pairs. */

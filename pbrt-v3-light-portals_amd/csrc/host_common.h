@@ -86,6 +86,15 @@ struct PlyMesh {
     bool hasN = false, hasUV = false;
 };
 void read_ply(const std::string& path, PlyMesh* out);
+
+// spectrum.cpp: spectral parameters reduced to RGB (RGBSpectrum build)
+float interpolate_spectrum_samples(const float* lambda, const float* vals, int n, float l);
+void xyz_to_rgb(const float xyz[3], float rgb[3]);
+void rgb_from_sampled(const float* lambda, const float* v, int n, float rgb[3]);
+void rgb_from_blackbody(float T, float scale, float rgb[3]);
+void blackbody_radiance(const float* lambda, int n, float T, float* Le);
+void copper_spectrum(bool k, float rgb[3]);  // metal's default eta (k=false) / k
+bool read_float_file(const std::string& path, std::vector<float>* values);
 // Shape "loopsubdiv" (shapes/loopsubdiv.cpp:137-398): refined limit-surface
 // mesh in object space -- positions, shading normals, triangle indices.
 void loop_subdivide(int levels, const std::vector<int>& indices, const std::vector<float>& P,

@@ -321,8 +321,8 @@ struct ParamSet {
         return true;
     }
     // FindOneSpectrum for the RGB build: "rgb"/"color" are RGB triples
-    // (RGBSpectrum::FromRGB); "spectrum"/"blackbody"/"xyz" need the CIE
-    // tables and are outside this round's subset.
+    // (RGBSpectrum::FromRGB); spectral types were reduced to "rgb" by
+    // spectral_to_rgb when the parameter list was parsed.
     bool spectrum(const char* n, float out[3]) const {
         for (auto it = params.rbegin(); it != params.rend(); ++it) {
             if (it->name != n) continue;
@@ -331,9 +331,6 @@ struct ParamSet {
                 for (int i = 0; i < 3; ++i) out[i] = (float)it->nums[i];
                 return true;
             }
-            if (it->type == "spectrum" || it->type == "blackbody" || it->type == "xyz")
-                throw PtError(PT_ERR_UNSUPPORTED, "spectral parameter \"" + it->type + " " + n +
-                                                      "\" needs the CIE tables (not in the supported subset)");
         }
         return false;
     }
@@ -452,8 +449,63 @@ class Loader {
                 }
             } else
                 add(v);
+            spectral_to_rgb(&p);
             ps.params.push_back(std::move(p));
         }
+    }
+
+    // The RGB build stores every spectral parameter as RGBSpectrum at parse
+    // time (paramset.cpp:122-208): "spectrum" wavelength/value pairs or SPD
+    // file names (FromSampled), "blackbody" (temperature, scale) pairs,
+    // "xyz" triples (FromXYZ).  Rewrite them as "rgb" parameters.
+    void spectral_to_rgb(Param* p) const {
+        std::vector<double> rgbs;
+        auto push = [&](const float c[3]) { for (int k = 0; k < 3; ++k) rgbs.push_back(c[k]); };
+        if (p->type == "spectrum") {
+            if (!p->strs.empty()) {
+                for (const std::string& name : p->strs) {
+                    std::string fn = (!name.empty() && name[0] == '/') ? name : searchDir_ + name;
+                    std::vector<float> vals;
+                    float c[3] = {0, 0, 0};
+                    if (!read_float_file(fn, &vals)) {
+                        std::fprintf(stderr, "Warning: Unable to read SPD file \"%s\".  Using black distribution.\n",
+                                     fn.c_str());
+                    } else {
+                        std::vector<float> wl, v;
+                        for (size_t j = 0; j + 1 < vals.size(); j += 2) wl.push_back(vals[j]), v.push_back(vals[j + 1]);
+                        rgb_from_sampled(wl.data(), v.data(), (int)wl.size(), c);
+                    }
+                    push(c);
+                }
+            } else {
+                if (p->nums.size() % 2) throw PtError(PT_ERR_PARSE, "spectrum \"" + p->name + "\" needs wavelength/value pairs");
+                std::vector<float> wl, v;
+                for (size_t j = 0; j < p->nums.size(); j += 2) wl.push_back((float)p->nums[j]), v.push_back((float)p->nums[j + 1]);
+                float c[3];
+                rgb_from_sampled(wl.data(), v.data(), (int)wl.size(), c);
+                push(c);
+            }
+        } else if (p->type == "blackbody") {
+            if (p->nums.size() % 2) throw PtError(PT_ERR_PARSE, "blackbody \"" + p->name + "\" needs (T, scale) pairs");
+            for (size_t j = 0; j < p->nums.size(); j += 2) {
+                float c[3];
+                rgb_from_blackbody((float)p->nums[j], (float)p->nums[j + 1], c);
+                push(c);
+            }
+        } else if (p->type == "xyz") {
+            if (p->nums.size() % 3) throw PtError(PT_ERR_PARSE, "xyz \"" + p->name + "\" needs triples");
+            for (size_t j = 0; j < p->nums.size(); j += 3) {
+                const float xyz[3] = {(float)p->nums[j], (float)p->nums[j + 1], (float)p->nums[j + 2]};
+                float c[3];
+                xyz_to_rgb(xyz, c);
+                push(c);
+            }
+        } else {
+            return;
+        }
+        p->type = "rgb";
+        p->nums = std::move(rgbs);
+        p->strs.clear();
     }
 
     std::vector<float> read_nums(Tokenizer& tk, int n) {
@@ -637,8 +689,7 @@ class Loader {
             m.sigma = sigma;
         } else if (name == "metal") {
             // CreateMetalMaterial (metal.cpp:113-131).  The default eta/k are
-            // copper spectra (Spectrum::FromSampled needs the CIE tables), so
-            // both must be given as rgb here.
+            // the measured copper spectra reduced by FromSampled (metal.cpp:116-122).
             m.kind = PT_MAT_METAL;
             for (const char* tex : {"eta", "k", "roughness", "uroughness", "vroughness", "bumpmap"})
                 if (gs_.materialParams.find(tex, {"texture"}) || shapeParams.find(tex, {"texture"}))
@@ -648,8 +699,8 @@ class Loader {
             hasEta = shapeParams.spectrum("eta", eta) || hasEta;
             bool hasK = gs_.materialParams.spectrum("k", k);
             hasK = shapeParams.spectrum("k", k) || hasK;
-            if (!hasEta || !hasK)
-                throw PtError(PT_ERR_UNSUPPORTED, "metal needs rgb \"eta\" and \"k\" (the copper default is spectral)");
+            if (!hasEta) copper_spectrum(false, eta);
+            if (!hasK) copper_spectrum(true, k);
             const float rough = f1("roughness", .01f, nullptr, shapeParams);
             bool hu = false, hv = false;
             float ur = f1("uroughness", 0.f, &hu, shapeParams), vr = f1("vroughness", 0.f, &hv, shapeParams);

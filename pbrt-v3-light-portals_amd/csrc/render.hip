@@ -1243,6 +1243,24 @@ pt_status pt_debug_libm_trig(int n, const float* x, float* sin_out, float* cos_o
         }
     });
 }
+pt_status pt_debug_spectrum(int kind, int n, const float* vals, float* out) {
+    return guarded([&] {
+        if (!vals || !out || n < 0) throw PtError(PT_ERR_INVALID_ARG, "pt_debug_spectrum: bad arguments");
+        if (kind == 0) {
+            std::vector<float> wl(n), v(n);
+            for (int i = 0; i < n; ++i) wl[i] = vals[2 * i], v[i] = vals[2 * i + 1];
+            rgb_from_sampled(wl.data(), v.data(), n, out);
+        } else if (kind == 1) {
+            rgb_from_blackbody(vals[0], vals[1], out);
+        } else if (kind == 2) {
+            xyz_to_rgb(vals, out);
+        } else if (kind == 3) {
+            for (int i = 0; i < n; ++i) blackbody_radiance(&vals[2 * i], 1, vals[2 * i + 1], &out[i]);
+        } else {
+            throw PtError(PT_ERR_INVALID_ARG, "pt_debug_spectrum: unknown kind");
+        }
+    });
+}
 pt_status pt_debug_halton(pt_scene* s, int n, const uint32_t* idx, const int32_t* dims, float* out) {
     return guarded([&] {
         DBuf<uint32_t> di; DBuf<int> dd; DBuf<float> o;

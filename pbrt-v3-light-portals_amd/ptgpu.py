@@ -81,6 +81,7 @@ def lib() -> ctypes.CDLL:
     L.pt_set_batch_slots.argtypes = [vp, ctypes.c_int64]
     L.pt_write_pfm.argtypes = [ctypes.c_char_p, f32p, i32, i32]
     L.pt_debug_libm_trig.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.pt_debug_spectrum.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp]
     L.pt_debug_halton.argtypes = [vp, ctypes.c_int, vp, vp, vp]
     L.pt_debug_pixel_offsets.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_camera_rays.argtypes = [vp, ctypes.c_int, vp, vp]
@@ -88,6 +89,17 @@ def lib() -> ctypes.CDLL:
     L.pt_debug_bsdf.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     _lib = L
     return L
+
+
+def spectrum_rgb(kind: int, vals, n_out: int = 3) -> np.ndarray:
+    """Host spectral reduction of the loader (pt_debug_spectrum): kind 0
+    (lambda, value) pairs -> RGB, 1 (T, scale) blackbody -> RGB, 2 xyz -> RGB,
+    3 (lambda, T) pairs -> Planck radiance."""
+    v = np.ascontiguousarray(vals, dtype=np.float32).ravel()
+    n = len(v) // 2 if kind in (0, 3) else len(v)
+    out = np.zeros(n if kind == 3 else n_out, dtype=np.float32)
+    _check(lib().pt_debug_spectrum(kind, n, v.ctypes.data, out.ctypes.data))
+    return out
 
 
 def _check(status: int) -> None:

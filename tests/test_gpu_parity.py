@@ -474,3 +474,20 @@ def test_portal_room_matches_oracle(tmp_path, strategy):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+def test_cornell_dielectric_matches_oracle(tmp_path):
+    """Config 3 (reference scenes/cornell_dielectric.pbrt: spectral walls and
+    lights reduced to RGB, specular + rough dispersive glass, infinite light,
+    gaussian filter; path maxdepth 5) at a reduced film: device == oracle bit
+    for bit, identical ray / node / primitive counts."""
+    from conftest import scene_variant
+    hs, sc = _scene(scene_variant(tmp_path, name="cornell_dielectric.pbrt", res=(64, 64), spp=16))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"cornell_dielectric: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert ref.mean() > 0
+    assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
