@@ -71,12 +71,13 @@ def test_metal_no_remap(tmp_path):
     assert list(m.alpha) == [F32(0.25), F32(0.25)]
 
 
-def test_metal_default_copper_is_refused(tmp_path):
+def test_metal_default_copper_loads(tmp_path):
+    """The copper default (metal.cpp:116-122) now reduces through the CIE
+    tables (values pinned in test_spectrum.py)."""
     p = scene_variant(tmp_path, extra=[("WorldEnd", 'Material "metal"\nShape "trianglemesh" "point P" '
                                                     '[0 0 0 1 0 0 1 1 0] "integer indices" [0 1 2]\nWorldEnd')])
-    with pytest.raises(ptgpu.PtError) as e:
-        ptgpu.HostScene(p)
-    assert e.value.status == 3  # PT_ERR_UNSUPPORTED
+    m = ptgpu.HostScene(p).materials()[-1]
+    assert m.kind == 2 and min(m.eta) > 0 and min(m.k) > 0
 
 
 def _cosine_hemisphere(u0, u1):
