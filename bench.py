@@ -86,7 +86,8 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
     _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=2 * threads)
     dt = time.perf_counter() - t0
     rate = st["samples"] / dt
-    tiles = int(max(2 * threads, min(4000, rate * seconds / (256 * 256))))
+    per_tile = st["samples"] / (2 * threads)
+    tiles = int(max(2 * threads, min(4000, rate * seconds / per_tile)))
     t0 = time.perf_counter()
     _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=tiles)
     dt = time.perf_counter() - t0
