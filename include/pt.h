@@ -346,6 +346,17 @@ pt_status pt_film_size(const pt_scene* scene, int32_t* width, int32_t* height);
 
 /* Film::WriteImage to a PFM file (imageio.cpp WritePFM). */
 pt_status pt_write_pfm(const char* path, const float* rgb, int32_t width, int32_t height);
+/* WriteImage (imageio.cpp:81-122): format by suffix (.exr half RGB with
+ * display window = full resolution and data window = [x0, x0+width) x
+ * [y0, y0+height); .pfm; .png / .tga 8-bit gamma-corrected).  rgb is the
+ * cropped image, width x height x 3, row-major from the top. */
+pt_status pt_write_image(const char* path, const float* rgb, int32_t width, int32_t height, int32_t full_xres,
+                         int32_t full_yres, int32_t x0, int32_t y0);
+/* Film::WriteImage (film.cpp:169-211 + the write above) for a rendered scene:
+ * rgb = pt_render output; the cropped pixel bounds come from desc->film. */
+pt_status pt_write_film_image(const pt_scene_desc* desc, const char* path, const float* rgb);
+/* Film "filename" of a loaded scene (film.cpp CreateFilm; default "pbrt.exr"). */
+const char* pt_host_scene_film_filename(const pt_host_scene* hs);
 
 /* ---- test hooks (used by the parity tests; not part of the render path) ---- */
 /* The shared host/device sinf/cosf port used by ConcentricSampleDisk,

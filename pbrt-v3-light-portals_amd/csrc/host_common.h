@@ -62,6 +62,7 @@ struct pt_host_scene_impl;
 pt_host_scene_impl* load_pbrt_file(const char* path);
 const pt_scene_desc* host_scene_desc(const pt_host_scene_impl* hs);
 void host_scene_free(pt_host_scene_impl* hs);
+const char* host_scene_film_filename(const pt_host_scene_impl* hs);
 
 // Axis-aligned box (Bounds3f)
 struct BBox {
@@ -86,6 +87,13 @@ struct PlyMesh {
     bool hasN = false, hasUV = false;
 };
 void read_ply(const std::string& path, PlyMesh* out);
+
+// imageio.cpp: Film output (WriteImage by suffix)
+void write_image(const std::string& name, const float* rgb, int xres, int yres, int totalX, int totalY, int x0,
+                 int y0);
+void write_pfm(const std::string& name, const float* rgb, int xres, int yres);
+uint16_t float_to_half(float x);
+uint8_t to_byte(float v);
 
 // spectrum.cpp: spectral parameters reduced to RGB (RGBSpectrum build)
 float interpolate_spectrum_samples(const float* lambda, const float* vals, int n, float l);

@@ -372,6 +372,7 @@ struct pt_host_scene_impl {
     std::vector<pt_material> materials;
     std::vector<pt_light> lights;
     std::vector<pt_portal> portals;
+    std::string film_filename = "pbrt.exr";
     pt_scene_desc desc{};
 };
 
@@ -1062,6 +1063,7 @@ class Loader {
         d.bvh_max_prims = accel_.ps.int1("maxnodeprims", 4);
         // Film (film.cpp:213-252)
         if (film_.name != "image") throw PtError(PT_ERR_UNSUPPORTED, "film \"" + film_.name + "\"");
+        out_->film_filename = film_.ps.string1("filename", "pbrt.exr");  // CreateFilm (film.cpp:213-225)
         d.film.xres = film_.ps.int1("xresolution", 1280);
         d.film.yres = film_.ps.int1("yresolution", 720);
         d.film.crop[0] = 0; d.film.crop[1] = 1; d.film.crop[2] = 0; d.film.crop[3] = 1;
@@ -1182,6 +1184,7 @@ pt_host_scene_impl* load_pbrt_file(const char* path) {
 }
 
 const pt_scene_desc* host_scene_desc(const pt_host_scene_impl* hs) { return &hs->desc; }
+const char* host_scene_film_filename(const pt_host_scene_impl* hs) { return hs->film_filename.c_str(); }
 void host_scene_free(pt_host_scene_impl* hs) { delete hs; }
 
 }  // namespace pt

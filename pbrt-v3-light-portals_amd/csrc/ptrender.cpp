@@ -1,6 +1,8 @@
 // ptrender.cpp -- pbrt-style command line (src/main/pbrt.cpp:43-173 subset)
-// on top of the C ABI: ptrender [--outfile f.pfm] [--device N] [--quiet]
-// [--stats] scene.pbrt.  Output is PFM (Film::WriteImage, film.cpp:169-211).
+// on top of the C ABI: ptrender [--outfile f] [--device N] [--quiet]
+// [--stats] scene.pbrt.  The image goes to the Film's "filename" (default
+// pbrt.exr) unless --outfile overrides it (film.cpp:213-225); the suffix
+// picks EXR / PFM / PNG / TGA (Film::WriteImage -> WriteImage, imageio.cpp:81-122).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -10,12 +12,12 @@
 #include "../../include/pt.h"
 
 static void usage() {
-    std::fprintf(stderr, "usage: ptrender [--outfile file.pfm] [--device N] [--quiet] [--stats] scene.pbrt\n");
+    std::fprintf(stderr, "usage: ptrender [--outfile file.{exr,pfm,png,tga}] [--device N] [--quiet] [--stats] scene.pbrt\n");
     std::exit(1);
 }
 
 int main(int argc, char** argv) {
-    std::string out = "pbrt.pfm", scene;
+    std::string out, scene;
     int device = 0;
     bool quiet = false, stats = false;
     for (int i = 1; i < argc; ++i) {
@@ -49,7 +51,8 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "ptrender: %s\n", pt_last_error());
         return 1;
     }
-    if (pt_write_pfm(out.c_str(), rgb.data(), w, h) != PT_OK) {
+    if (out.empty()) out = pt_host_scene_film_filename(hs);
+    if (pt_write_film_image(pt_host_scene_desc(hs), out.c_str(), rgb.data()) != PT_OK) {
         std::fprintf(stderr, "ptrender: %s\n", pt_last_error());
         return 1;
     }

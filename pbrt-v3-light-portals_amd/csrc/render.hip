@@ -1030,6 +1030,9 @@ pt_status pt_load_pbrt(const char* path, pt_host_scene** out) {
 const pt_scene_desc* pt_host_scene_desc(const pt_host_scene* hs) {
     return hs ? host_scene_desc((const pt_host_scene_impl*)hs) : nullptr;
 }
+const char* pt_host_scene_film_filename(const pt_host_scene* hs) {
+    return hs ? host_scene_film_filename((const pt_host_scene_impl*)hs) : nullptr;
+}
 void pt_host_scene_free(pt_host_scene* hs) {
     if (hs) host_scene_free((pt_host_scene_impl*)hs);
 }
@@ -1225,12 +1228,27 @@ pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
 pt_status pt_write_pfm(const char* path, const float* rgb, int32_t width, int32_t height) {
     return guarded([&] {
         if (!path || !rgb || width <= 0 || height <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
-        FILE* f = std::fopen(path, "wb");
-        if (!f) throw PtError(PT_ERR_IO, std::string("cannot open ") + path);
-        std::fprintf(f, "PF\n%d %d\n-1\n", width, height);  // little endian (imageio.cpp WritePFM)
-        for (int y = height - 1; y >= 0; --y)
-            std::fwrite(rgb + (size_t)3 * width * y, sizeof(float), (size_t)3 * width, f);
-        std::fclose(f);
+        write_pfm(path, rgb, width, height);
+    });
+}
+
+pt_status pt_write_image(const char* path, const float* rgb, int32_t width, int32_t height, int32_t full_xres,
+                         int32_t full_yres, int32_t x0, int32_t y0) {
+    return guarded([&] {
+        if (!path || !rgb || width <= 0 || height <= 0 || x0 < 0 || y0 < 0 || x0 + width > full_xres ||
+            y0 + height > full_yres)
+            throw PtError(PT_ERR_INVALID_ARG, "pt_write_image: bad bounds");
+        write_image(path, rgb, width, height, full_xres, full_yres, x0, y0);
+    });
+}
+pt_status pt_write_film_image(const pt_scene_desc* d, const char* path, const float* rgb) {
+    return guarded([&] {
+        if (!d || !path || !rgb) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        const pt_film_desc& f = d->film;
+        const int x0 = (int)std::ceil((float)f.xres * f.crop[0]), x1 = (int)std::ceil((float)f.xres * f.crop[1]);
+        const int y0 = (int)std::ceil((float)f.yres * f.crop[2]), y1 = (int)std::ceil((float)f.yres * f.crop[3]);
+        if (x1 <= x0 || y1 <= y0) throw PtError(PT_ERR_INVALID_ARG, "empty film crop");
+        write_image(path, rgb, x1 - x0, y1 - y0, f.xres, f.yres, x0, y0);
     });
 }
 

@@ -80,6 +80,10 @@ def lib() -> ctypes.CDLL:
     L.pt_film_size_host.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_set_batch_slots.argtypes = [vp, ctypes.c_int64]
     L.pt_write_pfm.argtypes = [ctypes.c_char_p, f32p, i32, i32]
+    L.pt_write_image.argtypes = [ctypes.c_char_p, f32p, i32, i32, i32, i32, i32, i32]
+    L.pt_write_film_image.argtypes = [vp, ctypes.c_char_p, f32p]
+    L.pt_host_scene_film_filename.argtypes = [vp]
+    L.pt_host_scene_film_filename.restype = ctypes.c_char_p
     L.pt_debug_libm_trig.argtypes = [ctypes.c_int, vp, vp, vp]
     L.pt_debug_spectrum.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp]
     L.pt_debug_halton.argtypes = [vp, ctypes.c_int, vp, vp, vp]
@@ -221,6 +225,18 @@ class HostScene:
         w, h = ctypes.c_int32(), ctypes.c_int32()
         _check(lib().pt_film_size_host(self.desc, ctypes.byref(w), ctypes.byref(h)))
         return w.value, h.value
+
+    @property
+    def film_filename(self) -> str:
+        return lib().pt_host_scene_film_filename(self._h).decode()
+
+    def write_image(self, rgb: np.ndarray, path: Optional[str] = None) -> str:
+        """Film::WriteImage of a rendered (h, w, 3) image to `path` (default:
+        the scene's Film "filename"); returns the path written."""
+        rgb = np.ascontiguousarray(rgb, np.float32)
+        path = path or self.film_filename
+        _check(lib().pt_write_film_image(self.desc, os.fsencode(path), _fptr(rgb)))
+        return path
 
     def resolve(self, accum: np.ndarray) -> np.ndarray:
         """Film::WriteImage of an (h, w, 4) XYZ+weight accumulation -- host only."""
@@ -366,6 +382,14 @@ def write_pfm(path: str, rgb: np.ndarray) -> None:
     rgb = np.ascontiguousarray(rgb, np.float32)
     h, w = rgb.shape[:2]
     _check(lib().pt_write_pfm(os.fsencode(path), _fptr(rgb), w, h))
+
+
+def write_image(path: str, rgb: np.ndarray, full_res=None, offset=(0, 0)) -> None:
+    """WriteImage by suffix (.exr/.pfm/.png/.tga) of a cropped (h, w, 3) image."""
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    h, w = rgb.shape[:2]
+    fw, fh = full_res or (w, h)
+    _check(lib().pt_write_image(os.fsencode(path), _fptr(rgb), w, h, fw, fh, offset[0], offset[1]))
 
 
 def exported_symbols() -> list:
