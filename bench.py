@@ -38,6 +38,9 @@ CONFIGS = {
            "reference scenes/cornell_dielectric.pbrt (spectral params reduced to RGB) with Integrator path, 1024 spp"),
     "c4": ("portal_room.pbrt", "portal room (config 4)", "path maxdepth 8",
            "synthetic (scenes/portal_room.pbrt from scripts/make_portal_room.py: room + 4 portals + sky; Halton)"),
+    "c5": ("killeroo_atrium.pbrt", "killeroo atrium 10M tris (config 5)", "path maxdepth 5",
+           "synthetic (scenes/killeroo_atrium.pbrt from scripts/make_atrium.py: 300 loop-subdivided killeroos, "
+           "9.98M triangles, skylight portal; Halton)"),
 }
 
 
@@ -48,7 +51,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="c2: the headline workload (default); c3: cornell_dielectric (BASELINE configs[2]); "
-                         "c4: portal room (BASELINE configs[3])")
+                         "c4: portal room (BASELINE configs[3]); c5: 10M-triangle atrium (BASELINE configs[4])")
     ap.add_argument("--scene", default="", help="override the config's scene file")
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per rank (0 = scene)")
     ap.add_argument("--res", default="", help="override WxH")
@@ -71,6 +74,9 @@ def scene_text(args) -> str:
         txt = re.sub(r'"integer pixelsamples" \[\d+\]', '"integer pixelsamples" [%d]' % args.spp, txt)
     if args.strategy:
         txt = re.sub(r'"string strategy" "\w+"', '"string strategy" "%s"' % args.strategy, txt)
+    # the copy is written to TMPDIR: keep relative Includes resolving against scenes/
+    sdir = os.path.dirname(os.path.abspath(args.scene)) if args.scene else os.path.join(REPO, "scenes")
+    txt = re.sub(r'Include "(?!/)([^"]+)"', lambda m: 'Include "%s/%s"' % (sdir, m.group(1)), txt)
     return txt
 
 

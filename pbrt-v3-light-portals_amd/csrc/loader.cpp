@@ -1120,8 +1120,17 @@ class Loader {
         d.sampler.spp = sampler_.ps.int1("pixelsamples", 16);
         d.sampler.sample_pixel_center = sampler_.ps.bool1("samplepixelcenter", false) ? 1 : 0;
         // Integrator (path.cpp:191-214, directlighting.cpp:86-118)
+        std::string lsDefault = "uniform";  // the fork's PathIntegrator default (path.cpp:210-211)
+        bool noRR = false;
         if (integrator_.name == "path") {
             d.integrator.kind = PT_INTEGRATOR_PATH;
+        } else if (integrator_.name == "mypath") {
+            // MyPathIntegrator (mypath.cpp): PathIntegrator::Li without the
+            // Russian-roulette block (path.cpp:177-185), default light
+            // strategy "spatial" (mypath.cpp:169-170).
+            d.integrator.kind = PT_INTEGRATOR_PATH;
+            noRR = true;
+            lsDefault = "spatial";
         } else if (integrator_.name == "directlighting") {
             d.integrator.kind = PT_INTEGRATOR_DIRECT;
             const std::string st = integrator_.ps.string1("strategy", "all");
@@ -1136,10 +1145,13 @@ class Loader {
             throw PtError(PT_ERR_UNSUPPORTED, "integrator \"" + integrator_.name + "\"");
         d.integrator.max_depth = integrator_.ps.int1("maxdepth", 5);
         d.integrator.rr_threshold = integrator_.ps.float1("rrthreshold", 1.f);
-        std::string ls = integrator_.ps.string1("lightsamplestrategy", "uniform");
-        if (ls == "uniform") d.integrator.light_strategy = PT_LIGHTS_UNIFORM;
+        // no RR: `maxComp(beta * etaScale) < -inf` never holds, so the block never runs
+        if (noRR) d.integrator.rr_threshold = -kInf;
+        // CreateLightSampleDistribution (lightdistrib.cpp:46-66): one light is always uniform
+        std::string ls = integrator_.ps.string1("lightsamplestrategy", lsDefault);
+        if (ls == "uniform" || out_->lights.size() == 1) d.integrator.light_strategy = PT_LIGHTS_UNIFORM;
         else if (ls == "power") d.integrator.light_strategy = PT_LIGHTS_POWER;
-        else throw PtError(PT_ERR_UNSUPPORTED, "lightsamplestrategy \"" + ls + "\"");
+        else throw PtError(PT_ERR_UNSUPPORTED, "lightsamplestrategy \"" + ls + "\" with several lights");
         if (const Param* pb = integrator_.ps.find("pixelbounds", {"integer"})) {
             if (pb->nums.size() == 4) {
                 d.integrator.has_pixel_bounds = 1;

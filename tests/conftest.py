@@ -50,6 +50,9 @@ def scene_variant(tmp_path, name="portal_cornell.pbrt", res=None, spp=None, stra
     if extra:
         for a, b in extra:
             txt = txt.replace(a, b)
+    import re
+    # the variant lives elsewhere: keep relative Includes resolving against scenes/
+    txt = re.sub(r'Include "(?!/)([^"]+)"', lambda m: 'Include "%s/%s"' % (SCENES, m.group(1)), txt)
     p = os.path.join(str(tmp_path), "v_%s_%s_%s_%s_%s" % (res, spp, strategy, maxdepth, name))
     p = p.replace(" ", "").replace("(", "").replace(")", "").replace(",", "x")
     with open(p, "w") as f:

@@ -4,6 +4,8 @@ match within the north_star tolerance (per-pixel RMSE < 1e-4 of the image,
 relative to its mean for the unbounded 'projection' estimator) -- and the
 renders are in fact required to be bit-identical, since the device performs
 the oracle's float operations in the oracle's order."""
+import os
+
 import numpy as np
 import pytest
 
@@ -488,6 +490,54 @@ def test_cornell_dielectric_matches_oracle(tmp_path):
     print(f"cornell_dielectric: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
     assert ref.mean() > 0
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
+
+
+@pytest.mark.parametrize("integrator", ["mypath", "directlighting"])
+def test_killeroo_simple_matches_oracle(tmp_path, integrator):
+    """Config 1 scene (reference scenes/killeroo-simple.pbrt: Loop-subdivided
+    killeroos, plastic, sphere area light) as written ("mypath": no Russian
+    roulette) and with the DirectLighting integrator config 1 names, at a
+    reduced film: device == oracle bit for bit."""
+    from conftest import scene_variant
+    extra = [('Integrator "mypath" "integer maxdepth" 3', 'Integrator "directlighting"')] \
+        if integrator == "directlighting" else None
+    hs, sc = _scene(scene_variant(tmp_path, name="killeroo-simple.pbrt", res=(48, 48), spp=4, extra=extra))
+    assert ptgpu.integrator_desc(hs).kind == (1 if integrator == "directlighting" else 0)
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"killeroo/{integrator}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert ref.mean() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
+
+
+def test_killeroo_atrium_matches_oracle(tmp_path):
+    """Config 5 scene family (scripts/make_atrium.py: Loop-subdivided
+    killeroos in a skylight-portal atrium) with 12 copies (0.4 M triangles,
+    same code path as the 300-copy / 10 M-triangle bench scene) at a reduced
+    film: device == oracle bit for bit, identical traversal counters."""
+    import re
+    import subprocess
+    import sys
+    from conftest import REPO, SCENES
+    src = tmp_path / "atrium12.pbrt"
+    subprocess.check_call([sys.executable, os.path.join(REPO, "scripts", "make_atrium.py"), str(src),
+                           "--copies", "12"])
+    txt = src.read_text()
+    txt = re.sub(r'Include "([^"]+)"', lambda m: 'Include "%s/%s"' % (SCENES, m.group(1)), txt)
+    txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [64]', txt)
+    txt = re.sub(r'"integer yresolution" \[\d+\]', '"integer yresolution" [36]', txt)
+    txt = re.sub(r'"integer pixelsamples" \[\d+\]', '"integer pixelsamples" [4]', txt)
+    src.write_text(txt)
+    hs, sc = _scene(str(src))
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"atrium12: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert ref.mean() > 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k

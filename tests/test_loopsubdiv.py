@@ -272,3 +272,16 @@ def test_loopsubdiv_renders(tmp_path):
     hs = ptgpu.HostScene(_scene(tmp_path, P, idx, 2, material='Material "plastic" "rgb Kd" [0.4 0.2 0.2]'))
     img, st = pyoracle.render(hs.desc, nthreads=4)
     assert np.isfinite(img).all() and img.mean() > 0
+
+
+def test_killeroo_simple_shape_count():
+    """BASELINE config 1 scene (reference scenes/killeroo-simple.pbrt): two
+    `loopsubdiv nlevels 1` killeroos + 4 quad triangles + 1 sphere.  The
+    reference's own run counted 66,533 shapes (SURVEY.md §8(d) C5 [probe]),
+    which pins the subdivided topology: 2 x 33,264 triangles."""
+    from conftest import REPO
+    hs = ptgpu.HostScene(os.path.join(REPO, "scenes", "killeroo-simple.pbrt"))
+    d = ptgpu._desc_prefix.from_address(hs.desc)
+    assert d.n_prims == 66533 and d.n_triangles == 66532
+    it = ptgpu.integrator_desc(hs)
+    assert it.kind == 0 and it.rr_threshold == float("-inf")  # "mypath": PathIntegrator without RR
