@@ -2,6 +2,8 @@
 // reference function (file:line cited) with the same float operation order.
 #pragma once
 
+#undef PT_FILE_ID
+#define PT_FILE_ID 1  // PT_IDX source tag
 #include "device.h"
 
 namespace pt {
@@ -182,10 +184,10 @@ __device__ __forceinline__ bool tri_hit(V3 p0, V3 p1, V3 p2, const Ray& ray, flo
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ bool plane_test(const DevPlane& pl, const Ray& ray, float* tHit, V3* pHitObj) {
     Ray rT = xf_ray_keep_tmax(pl.w2o, ray);
-    float t = (pl.lo[pl.ax] - rT.o[pl.ax]) / rT.d[pl.ax];
+    float t = (pl.lo_a - rT.o[pl.ax]) / rT.d[pl.ax];
     V3 pHit = rT.o + t * rT.d;
-    if (pHit[pl.ax0] > pl.lo[pl.ax0] && pHit[pl.ax0] < pl.hi[pl.ax0] && pHit[pl.ax1] > pl.lo[pl.ax1] &&
-        pHit[pl.ax1] < pl.hi[pl.ax1] && t < rT.tmax) {
+    if (pHit[pl.ax0] > pl.lo_a0 && pHit[pl.ax0] < pl.hi_a0 && pHit[pl.ax1] > pl.lo_a1 &&
+        pHit[pl.ax1] < pl.hi_a1 && t < rT.tmax) {
         *tHit = t;
         *pHitObj = pHit;
         return true;
@@ -206,8 +208,8 @@ __device__ __forceinline__ V3 vload3(const float* a, int i) { return v3(a[3 * i]
 // reference would reject (it never does for the primitive that won in the
 // traversal, which already applied the same tests).
 __device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si) {
-    const pt_triangle tr = sc.tris[ti];
-    V3 p0 = vload3(sc.P, tr.v[0]), p1 = vload3(sc.P, tr.v[1]), p2 = vload3(sc.P, tr.v[2]);
+    const pt_triangle tr = sc.tris[PT_IDX(ti, sc.n_tris)];
+    V3 p0 = vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)), p1 = vload3(sc.P, PT_IDX(tr.v[1], sc.n_verts)), p2 = vload3(sc.P, PT_IDX(tr.v[2], sc.n_verts));
     Ray r2 = ray;
     r2.tmax = kInf;
     float t, b0, b1, b2;
@@ -215,7 +217,7 @@ __device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ra
     float uv[3][2];
     bool hasUV = (tr.flags & PT_TRI_HAS_UV) && sc.UV;
     if (hasUV) {
-        for (int i = 0; i < 3; ++i) { uv[i][0] = sc.UV[2 * tr.v[i]]; uv[i][1] = sc.UV[2 * tr.v[i] + 1]; }
+        for (int i = 0; i < 3; ++i) { uv[i][0] = sc.UV[2 * PT_IDX(tr.v[i], sc.n_verts)]; uv[i][1] = sc.UV[2 * PT_IDX(tr.v[i], sc.n_verts) + 1]; }
     } else {
         uv[0][0] = 0; uv[0][1] = 0; uv[1][0] = 1; uv[1][1] = 0; uv[2][0] = 1; uv[2][1] = 1;
     }
@@ -253,13 +255,13 @@ __device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ra
     if (hasN || hasS) {
         V3 ns;
         if (hasN) {
-            ns = (b0 * vload3(sc.N, tr.v[0]) + b1 * vload3(sc.N, tr.v[1])) + b2 * vload3(sc.N, tr.v[2]);
+            ns = (b0 * vload3(sc.N, PT_IDX(tr.v[0], sc.n_verts)) + b1 * vload3(sc.N, PT_IDX(tr.v[1], sc.n_verts))) + b2 * vload3(sc.N, PT_IDX(tr.v[2], sc.n_verts));
             ns = (len2(ns) > 0) ? normalize(ns) : si->n;
         } else
             ns = si->n;
         V3 ss;
         if (hasS) {
-            ss = (b0 * vload3(sc.S, tr.v[0]) + b1 * vload3(sc.S, tr.v[1])) + b2 * vload3(sc.S, tr.v[2]);
+            ss = (b0 * vload3(sc.S, PT_IDX(tr.v[0], sc.n_verts)) + b1 * vload3(sc.S, PT_IDX(tr.v[1], sc.n_verts))) + b2 * vload3(sc.S, PT_IDX(tr.v[2], sc.n_verts));
             ss = (len2(ss) > 0) ? normalize(ss) : normalize(dpdu);
         } else
             ss = normalize(dpdu);
@@ -412,18 +414,18 @@ __device__ __forceinline__ bool sphere_surface(const DevSphere& s, const Ray& ra
 template <bool kSph = true>
 __device__ __forceinline__ bool shape_test(const DevScene& sc, uint32_t flags, int idx, const Ray& ray, float* t) {
     V3 ph;
-    if (kSph && (flags & kPrimSphere)) return sphere_test(sc.spheres[idx], ray, t, &ph);
-    return plane_test(sc.planes[idx], ray, t, &ph);
+    if (kSph && (flags & kPrimSphere)) return sphere_test(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, t, &ph);
+    return plane_test(sc.planes[PT_IDX(idx, sc.n_planes)], ray, t, &ph);
 }
 
 template <bool kSph = true>
 __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
-    float4 r0 = sc.prims[3 * prim];
-    float4 r1 = sc.prims[3 * prim + 1];
+    float4 r0 = sc.prims[3 * PT_IDX(prim, sc.n_prims)];
+    float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
-    bool ok = (kSph && (flags & kPrimSphere)) ? sphere_surface(sc.spheres[idx], ray, si)
-              : (flags & kPrimPlane) ? plane_surface(sc.planes[idx], ray, si)
+    bool ok = (kSph && (flags & kPrimSphere)) ? sphere_surface(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, si)
+              : (flags & kPrimPlane) ? plane_surface(sc.planes[PT_IDX(idx, sc.n_planes)], ray, si)
                                      : tri_surface(sc, idx, ray, si);
     si->prim = prim;
     return ok;
@@ -431,18 +433,18 @@ __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const R
 
 template <bool kSph = true>
 __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
-    float4 r0 = sc.prims[3 * prim];
-    float4 r1 = sc.prims[3 * prim + 1];
+    float4 r0 = sc.prims[3 * PT_IDX(prim, sc.n_prims)];
+    float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
     if (kSph && (flags & kPrimSphere)) {
-        *material = sc.spheres[idx].material;
-        *light = sc.spheres[idx].area_light;
+        *material = sc.spheres[PT_IDX(idx, sc.n_spheres)].material;
+        *light = sc.spheres[PT_IDX(idx, sc.n_spheres)].area_light;
     } else if (flags & kPrimPlane) {
-        *material = sc.planes[idx].material;
-        *light = sc.planes[idx].area_light;
+        *material = sc.planes[PT_IDX(idx, sc.n_planes)].material;
+        *light = sc.planes[PT_IDX(idx, sc.n_planes)].area_light;
     } else {
-        const pt_triangle& t = sc.tris[idx];
+        const pt_triangle& t = sc.tris[PT_IDX(idx, sc.n_tris)];
         *material = t.material;
         *light = t.area_light;
     }
@@ -936,7 +938,7 @@ __device__ __forceinline__ V3 plane_normal(const DevPlane& pl) {  // plane.cpp:7
     return r;
 }
 __device__ __forceinline__ bool plane_in_front(const DevPlane& pl, V3 p) {  // plane.cpp:109-115
-    return pl.facing_fw ? (p[pl.ax] > pl.lo[pl.ax]) : (p[pl.ax] < pl.lo[pl.ax]);
+    return pl.facing_fw ? (p[pl.ax] > pl.lo_a) : (p[pl.ax] < pl.lo_a);
 }
 __device__ __forceinline__ void plane_sample(const DevPlane& pl, float u0, float u1, V3* p, V3* n, V3* perr,
                                              float* pdf) {  // plane.cpp:57-72
@@ -952,22 +954,22 @@ __device__ __forceinline__ void plane_sample(const DevPlane& pl, float u0, float
 }
 __device__ __forceinline__ void tri_sample(const DevScene& sc, int ti, float u0, float u1, V3* p, V3* n, V3* perr,
                                            float* pdf) {  // triangle.cpp:584-609
-    const pt_triangle tr = sc.tris[ti];
+    const pt_triangle tr = sc.tris[PT_IDX(ti, sc.n_tris)];
     float su0 = sqrtf(u0);
     float b0 = 1 - su0, b1 = u1 * su0;
-    V3 p0 = vload3(sc.P, tr.v[0]), p1 = vload3(sc.P, tr.v[1]), p2 = vload3(sc.P, tr.v[2]);
+    V3 p0 = vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)), p1 = vload3(sc.P, PT_IDX(tr.v[1], sc.n_verts)), p2 = vload3(sc.P, PT_IDX(tr.v[2], sc.n_verts));
     float b2 = 1 - b0 - b1;
     *p = (b0 * p0 + b1 * p1) + b2 * p2;
     *n = normalize(cross(p1 - p0, p2 - p0));
     if ((tr.flags & PT_TRI_HAS_N) && sc.N) {
-        V3 ns = (b0 * vload3(sc.N, tr.v[0]) + b1 * vload3(sc.N, tr.v[1])) + b2 * vload3(sc.N, tr.v[2]);
+        V3 ns = (b0 * vload3(sc.N, PT_IDX(tr.v[0], sc.n_verts)) + b1 * vload3(sc.N, PT_IDX(tr.v[1], sc.n_verts))) + b2 * vload3(sc.N, PT_IDX(tr.v[2], sc.n_verts));
         *n = faceforward(*n, ns);
     } else if (((tr.flags & PT_TRI_REVERSE_ORIENTATION) != 0) ^ ((tr.flags & PT_TRI_SWAPS_HANDEDNESS) != 0)) {
         *n = *n * -1.f;
     }
     V3 pa = (vabs(b0 * p0) + vabs(b1 * p1)) + vabs(b2 * p2);
     *perr = gammaf(6) * pa;
-    *pdf = 1 / sc.tri_area[ti];
+    *pdf = 1 / sc.tri_area[PT_IDX(ti, sc.n_tris)];
 }
 
 // ----------------------------------------------------------------------------
@@ -1114,14 +1116,14 @@ __device__ __forceinline__ S3 area_sample_li(const DevScene& sc, const DevLight&
         return l.L / dist2(l.center, ref.p);
     }
     if (Ft<kFt>::sph && l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
-        sphere_sample_ref(sc.spheres[l.shape], ref, u0, u1, &p, &n, &pe, pdf);
+        sphere_sample_ref(sc.spheres[PT_IDX(l.shape, sc.n_spheres)], ref, u0, u1, &p, &n, &pe, pdf);
         if (*pdf == 0 || len2(p - ref.p) == 0) { *pdf = 0; return s3(0.f); }
         *wi = normalize(p - ref.p);
         *sp = p; *sn = n; *spe = pe;
         return area_L(l, n, -*wi);
     }
     if (l.kind == PT_LIGHT_DIFFUSE_AREA) tri_sample(sc, l.shape, u0, u1, &p, &n, &pe, pdf);
-    else plane_sample(sc.planes[l.shape], u0, u1, &p, &n, &pe, pdf);
+    else plane_sample(sc.planes[PT_IDX(l.shape, sc.n_planes)], u0, u1, &p, &n, &pe, pdf);
     V3 w = p - ref.p;
     if (len2(w) == 0) *pdf = 0;
     else {
@@ -1144,7 +1146,7 @@ __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight&
     SurfHit isl;
     bool ok;
     if (Ft<kFt>::sph && l.kind == PT_LIGHT_DIFFUSE_SPHERE) {  // Sphere::Pdf (sphere.cpp:303-315)
-        const DevSphere& s = sc.spheres[l.shape];
+        const DevSphere& s = sc.spheres[PT_IDX(l.shape, sc.n_spheres)];
         const V3 pOrigin = offset_ray_origin(ref.p, ref.perr, ref.n, s.center - ref.p);
         if (!(dist2(pOrigin, s.center) <= s.radius * s.radius)) {
             const float sinThetaMax2 = s.radius * s.radius / dist2(ref.p, s.center);
@@ -1157,7 +1159,7 @@ __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight&
         // Triangle::Intersect on this one triangle (tMax = Infinity).
         ok = tri_surface(sc, l.shape, r, &isl);
     } else {
-        ok = plane_surface(sc.planes[l.shape], r, &isl);
+        ok = plane_surface(sc.planes[PT_IDX(l.shape, sc.n_planes)], r, &isl);
     }
     if (!ok) return 0;
     float pdf = dist2(ref.p, isl.p) / (absdot(isl.n, -wi) * area);

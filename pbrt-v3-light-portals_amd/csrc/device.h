@@ -15,6 +15,9 @@ namespace pt {
 struct DevPlane {
     V3 lo, hi;
     int ax, ax0, ax1;
+    // lo/hi along (ax, ax0, ax1), so no bound is read from memory at a
+    // run-time component offset (plane.cpp:23-31, 109-115)
+    float lo_a, lo_a0, lo_a1, hi_a0, hi_a1;
     int facing_fw;
     int ro_xor_sh;
     int material;
@@ -60,6 +63,22 @@ constexpr uint32_t kPrimDegenerate = 2u;  // Triangle::Intersect always rejects 
 constexpr uint32_t kPrimSphere = 4u;      // Sphere
 constexpr uint32_t kPrimAnalytic = kPrimPlane | kPrimSphere;  // record holds a shape index, not vertices
 
+// PT_GUARDS (diagnostic build, `make guard`): scene-table indices on the
+// shading path are range-checked; the first failing check records
+// file_id * 100000 + line in g_pt_guard and index 0 is used instead of
+// faulting.  Production builds compile PT_IDX(i, n) to i.
+#ifdef PT_GUARDS
+__device__ unsigned int g_pt_guard;
+__device__ __forceinline__ int pt_idx(int i, int n, unsigned int where) {
+    if ((unsigned)i < (unsigned)n) return i;
+    atomicCAS(&g_pt_guard, 0u, where);
+    return 0;
+}
+#define PT_IDX(i, n) pt_idx((i), (n), PT_FILE_ID * 100000u + __LINE__)
+#else
+#define PT_IDX(i, n) (i)
+#endif
+
 struct DevScene {
     // BVH: 2 x float4 per LinearBVHNode; 3 x float4 per primitive in BVH order
     const float4* nodes;
@@ -77,6 +96,7 @@ struct DevScene {
     const pt_material* mats;
     const DevLight* lights;
     int n_lights;
+    int n_tris, n_planes, n_pplanes, n_spheres, n_mats, n_verts;  // table sizes (PT_GUARDS builds check against them)
     const float* ldist_func;
     const float* ldist_cdf;
     float ldist_int;

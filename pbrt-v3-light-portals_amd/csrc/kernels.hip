@@ -11,6 +11,8 @@
 // filter window -- deterministic, no float atomics.
 #include "devfuncs.h"
 #include "kernels.h"
+#undef PT_FILE_ID
+#define PT_FILE_ID 2  // PT_IDX source tag
 
 namespace pt {
 
@@ -605,7 +607,7 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
     prim_info<Ft<kFt>::sph>(sc, prim, &mat, &light);
     *lightOut = light;
     if (light < 0) return s3(0.f);
-    const DevLight& l = sc.lights[light];
+    const DevLight& l = sc.lights[PT_IDX(light, sc.n_lights)];
     if (l.two_sided) return l.L;
     SurfHit si;
     if (!surface_at<Ft<kFt>::sph>(sc, prim, ray, &si)) return s3(0.f);
@@ -645,8 +647,8 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
                 int lid;
                 const S3 le = hit_Le<kFt>(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
                 if (lid == nl) Li = le;
-            } else if (Ft<kFt>::inf && sc.lights[nl].kind == PT_LIGHT_INFINITE) {
-                Li = inf_Le(sc.lights[nl], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
+            } else if (Ft<kFt>::inf && sc.lights[PT_IDX(nl, sc.n_lights)].kind == PT_LIGHT_INFINITE) {
+                Li = inf_Le(sc.lights[PT_IDX(nl, sc.n_lights)], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
             }
             if (!is_black(Li)) {
                 const S3 f2 = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
@@ -678,8 +680,8 @@ __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int 
 template <int kFt>
 __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                            const SurfHit& it, const Bsdf& bsdf, float u10, float u11) {
-    const DevLight& l = sc.lights[lightIdx];
-    const DevPlane& lp = sc.planes[l.shape];
+    const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
+    const DevPlane& lp = sc.planes[PT_IDX(l.shape, sc.n_planes)];
     const uint32_t N = (uint32_t)ps.n;
     uint32_t flags = kNfPortal;
     if (l.strategy != PT_PORTAL_LIGHT) {
@@ -689,6 +691,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
         // so dist[i] is 1 for portals in front of the point and 0 otherwise; the
         // CDF entries are recomputed with the same sequential float sums.
         const int np = l.n_portals;
+        if (np > 0 && PT_IDX(l.first_portal + np - 1, sc.n_pplanes) != l.first_portal + np - 1) return false;
         const DevPlane* portals = sc.portal_planes + l.first_portal;
         int nvis = 0;
         for (int i = 0; i < np; ++i) nvis += plane_in_front(portals[i], pObj) ? 1 : 0;
@@ -711,7 +714,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
             sel = sel < 0 ? 0 : (sel > np - 1 ? np - 1 : sel);
             const float dsel = plane_in_front(portals[sel], pObj) ? dv : 0.f / sum;
             const float portalPdf = (funcInt > 0) ? dsel / (funcInt * np) : 0;
-            const DevPlane& pp = sc.portal_planes[l.first_portal + sel];
+            const DevPlane& pp = sc.portal_planes[PT_IDX(l.first_portal + sel, sc.n_pplanes)];
             if (plane_in_front(pp, pObj)) {
                 V3 wi = v3(0, 0, 0);
                 float pdf = 0;
@@ -728,8 +731,9 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                     const V3 dHi = normalize(it.p - lp.hi);
                     if (dLo.z == 0 || dHi.z == 0) pdf = 0;
                     else {
-                        const float tLo = (pp.lo[pp.ax] - lp.lo[lp.ax]) / dLo[lp.ax];
-                        const float tHi = (pp.lo[pp.ax] - lp.hi[lp.ax]) / dHi[lp.ax];
+                        const V3 lpLo = lp.lo, lpHi = lp.hi;
+                        const float tLo = (pp.lo_a - lpLo[lp.ax]) / dLo[lp.ax];
+                        const float tHi = (pp.lo_a - lpHi[lp.ax]) / dHi[lp.ax];
                         const V3 projLo = lp.lo + dLo * tLo;
                         const V3 projHi = lp.hi + dHi * tHi;
                         const V3 isectHi = vmax(pp.lo, projLo);
@@ -737,7 +741,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                         const float len0 = isectHi[pp.ax0] - isectLo[pp.ax0];
                         const float len1 = isectHi[pp.ax1] - isectLo[pp.ax1];
                         V3 sampled = v3(0, 0, 0);
-                        sampled.set(pp.ax, pp.lo[pp.ax]);
+                        sampled.set(pp.ax, pp.lo_a);
                         sampled.set(pp.ax0, isectLo[pp.ax0] + u10 * len0);
                         sampled.set(pp.ax1, isectLo[pp.ax1] + u10 * len1);
                         const V3 sampledWorld = xf_point(pp.w2o, sampled);
@@ -782,7 +786,7 @@ template <int kFt>
 __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                             const SurfHit& it, const Bsdf& bsdf, float ul0, float ul1, float us0,
                                             float us1) {
-    const DevLight& l = sc.lights[lightIdx];
+    const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
     const uint32_t N = (uint32_t)ps.n;
     uint32_t flags = kNfMis;
     V3 wi, sp, sn, spe;
@@ -839,9 +843,10 @@ template <int kFt>
 __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
                                            uint32_t* nrays, bool* keep, bool* overflow) {
     const uint32_t N = (uint32_t)ps.n;
+    *nrays = 0;
+    if (PT_IDX((int)slot, ps.n) != (int)slot) return;
     uint32_t st = ps.st[slot];
     S3 L = load_s3(ps.L, N, slot);
-    *nrays = 0;
     if (st & kStNee) {
         resolve_nee<kFt>(sc, ps, slot, &L);
         st &= ~kStNee;
@@ -858,13 +863,13 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         int mat = -1, light = -1;
         if (found) prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
         if (bounces == 0 || specular) {
-            if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[light], si.n, -ray.d) : s3(0.f));
+            if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[PT_IDX(light, sc.n_lights)], si.n, -ray.d) : s3(0.f));
             else if (Ft<kFt>::inf)
                 for (int li = 0; li < sc.n_lights; ++li)  // scene.infiniteLights, in light order
-                    if (sc.lights[li].kind == PT_LIGHT_INFINITE) L = L + beta * inf_Le(sc.lights[li], ray.d);
+                    if (sc.lights[PT_IDX(li, sc.n_lights)].kind == PT_LIGHT_INFINITE) L = L + beta * inf_Le(sc.lights[PT_IDX(li, sc.n_lights)], ray.d);
         }
         if (found && bounces < sc.max_depth) {
-            if (sc.mats[mat].kind == PT_MAT_NONE) {
+            if (sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_NONE) {
                 // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
                 const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
                 store_ray6(ps.ray, N, slot, r);
@@ -874,9 +879,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
-                const float wvl0 = Ft<kFt>::spec && sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
+                const float wvl0 = Ft<kFt>::spec && sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_DISPERSIVE_GLASS
                                        ? (float)400 + (float)300 * halton_dim(sc, dm.idx, sc.wvl_dim) : 550.f;
-                make_bsdf<kFt>(&sc.mats[mat], si, wvl0, &bsdf);
+                make_bsdf<kFt>(&sc.mats[PT_IDX(mat, sc.n_mats)], si, wvl0, &bsdf);
                 if (bsdf_num<kFt>(bsdf, kBxNonSpecular) > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
                     bool deferred = false;
@@ -885,12 +890,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                     if (sc.n_lights > 0) {
                         const float ul = dm.get1();
                         const int ln = find_interval(sc.ldist_cdf, sc.n_lights + 1, ul);
-                        lightPdf = (sc.ldist_int > 0) ? sc.ldist_func[ln] / (sc.ldist_int * sc.n_lights) : 0;
+                        lightPdf = (sc.ldist_int > 0) ? sc.ldist_func[PT_IDX(ln, sc.n_lights)] / (sc.ldist_int * sc.n_lights) : 0;
                         if (lightPdf != 0) {
                             haveLight = true;
                             const float uL0 = dm.get1(), uL1 = dm.get1();
                             const float uS0 = dm.get1(), uS1 = dm.get1();
-                            if (sc.lights[ln].kind == PT_LIGHT_PORTAL_AREA) {
+                            if (sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
                                 if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1)) {
                                     rays[(*nrays)++] = slot << 2 | kRayA;
                                     deferred = true;
@@ -1032,15 +1037,15 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
         surface_at<Ft<kFt>::sph>(sc, prim, r, &si);
         int mat, light;
         prim_info<Ft<kFt>::sph>(sc, prim, &mat, &light);
-        const float wvl0 = Ft<kFt>::spec && sc.mats[mat].kind == PT_MAT_DISPERSIVE_GLASS
+        const float wvl0 = Ft<kFt>::spec && sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_DISPERSIVE_GLASS
                                ? (float)400 + (float)300 * halton_dim(sc, dm.idx, sc.wvl_dim) : 550.f;
-        make_bsdf<kFt>(&sc.mats[mat], si, wvl0, &bsdf, false);
+        make_bsdf<kFt>(&sc.mats[PT_IDX(mat, sc.n_mats)], si, wvl0, &bsdf, false);
         haveV = true;
     };
     // one EstimateDirect: emits its rays, or yields Ld = 0 at once
     auto estimate = [&](int j, float uL0, float uL1, float uS0, float uS1) -> bool {
         vertex();
-        if (sc.lights[j].kind == PT_LIGHT_PORTAL_AREA) {
+        if (sc.lights[PT_IDX(j, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
             if (portal_nee<kFt>(sc, ps, slot, j, si, bsdf, uS0, uS1)) {
                 rays[(*nrays)++] = slot << 2 | kRayA;
                 return true;
@@ -1083,14 +1088,14 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
                     S3 Lm = s3(0.f);
                     if (Ft<kFt>::inf)
                         for (int li = 0; li < sc.n_lights; ++li)
-                            if (sc.lights[li].kind == PT_LIGHT_INFINITE) Lm = Lm + inf_Le(sc.lights[li], ray.d);
+                            if (sc.lights[PT_IDX(li, sc.n_lights)].kind == PT_LIGHT_INFINITE) Lm = Lm + inf_Le(sc.lights[PT_IDX(li, sc.n_lights)], ray.d);
                     Lc = Lm;
                     step = kDlReturn;
                     break;
                 }
                 int mat, light;
                 prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
-                if (sc.mats[mat].kind == PT_MAT_NONE) {  // Li(isect.SpawnRay(ray.d), depth)
+                if (sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_NONE) {  // Li(isect.SpawnRay(ray.d), depth)
                     const Ray r{offset_ray_origin(h.p, h.perr, h.n, ray.d), ray.d, kInf};
                     store_ray6(ps.ray, N, slot, r);
                     st |= kStCont;
@@ -1102,7 +1107,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
                 fr(d, kFrPrim) = __int_as_float(hp);
                 haveV = false;
                 vertex();
-                const S3 Le = light >= 0 ? area_L(sc.lights[light], si.n, si.wo) : s3(0.f);  // isect.Le(wo)
+                const S3 Le = light >= 0 ? area_L(sc.lights[PT_IDX(light, sc.n_lights)], si.n, si.wo) : s3(0.f);  // isect.Le(wo)
                 set3(d, kFrL, s3(0.f) + Le);
                 if (sc.n_lights > 0) {
                     if (sc.dl_strategy == PT_DIRECT_ALL) {
@@ -1122,7 +1127,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
                     step = kDlSpecR;
                     break;
                 }
-                const int n = sc.lights[j].n_samples;
+                const int n = sc.lights[PT_IDX(j, sc.n_lights)].n_samples;
                 int aoff = I[kDlAoff * N + slot];
                 const int a1 = aoff < sc.dl_arrays ? aoff++ : -1;
                 const int a2 = aoff < sc.dl_arrays ? aoff++ : -1;
@@ -1423,7 +1428,7 @@ __global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float
     SurfHit si{};
     si.n = v3(0, 0, 1); si.sn = v3(0, 0, 1); si.sdpdu = v3(1, 0, 0);
     Bsdf b;
-    make_bsdf(&sc.mats[mat], si, 550.f, &b, sc.integrator != PT_INTEGRATOR_DIRECT);
+    make_bsdf(&sc.mats[PT_IDX(mat, sc.n_mats)], si, 550.f, &b, sc.integrator != PT_INTEGRATOR_DIRECT);
     const V3 wo = v3(a[0], a[1], a[2]), wi = v3(a[3], a[4], a[5]);
     float* o = out + 8 * i;
     S3 f = s3(0.f);

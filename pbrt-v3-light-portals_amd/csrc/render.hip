@@ -461,6 +461,11 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         pl.ax = axis;
         pl.ax0 = axis == 2 ? 0 : (axis == 0 ? 1 : 2);
         pl.ax1 = axis == 2 ? 1 : (axis == 0 ? 2 : 0);
+        pl.lo_a = pl.lo[pl.ax];
+        pl.lo_a0 = pl.lo[pl.ax0];
+        pl.lo_a1 = pl.lo[pl.ax1];
+        pl.hi_a0 = pl.hi[pl.ax0];
+        pl.hi_a1 = pl.hi[pl.ax1];
         pl.facing_fw = ro ? 0 : 1;
         pl.ro_xor_sh = (ro != sh) ? 1 : 0;
         pl.material = material;
@@ -675,6 +680,12 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     ds.mats = s->mats.p;
     ds.lights = s->lights.p;
     ds.n_lights = nl;
+    ds.n_tris = d->n_triangles;
+    ds.n_planes = d->n_planes;
+    ds.n_pplanes = d->n_portals;
+    ds.n_spheres = d->n_spheres;
+    ds.n_mats = d->n_materials;
+    ds.n_verts = d->n_vertices;
     ds.ldist_func = s->lfunc.p;
     ds.ldist_cdf = s->lcdf.p;
     ds.ldist_int = funcInt;
@@ -841,6 +852,16 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     };
     double trace_ms = 0;
     size_t tcount = 0;
+    // PT_SYNC_CHECK=1 (diagnostics): synchronise after every launch so a
+    // device fault is reported against the kernel and bounce that raised it.
+    const bool syncCheck = std::getenv("PT_SYNC_CHECK") != nullptr;
+    auto sync_check = [&](const char* what, int it) {
+        if (!syncCheck) return;
+        const hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess)
+            throw PtError(PT_ERR_DEVICE, std::string(what) + " (bounce iteration " + std::to_string(it) + "): " +
+                                             hipGetErrorString(e));
+    };
     HIPCHK(hipEventRecord(ev0, stream));
     uint32_t* counts = w.counts.p;
     uint32_t host_counts[8];
@@ -852,6 +873,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                                stream, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
             hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
             HIPCHK(hipGetLastError());
+            sync_check("k_camera", 0);
             uint32_t *rq_in = w.rq0.p, *rq_out = w.rq1.p, *pq_in = w.pq0.p, *pq_out = w.pq1.p;
             uint32_t nrays = nb, npaths = nb;
             int iter = 0;
@@ -884,12 +906,14 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                                            counts + 0, w.spill.p, w.stats.p);
                     HIPCHK(hipEventRecord(e.second, stream));
                     rr.launches++;
+                    sync_check("k_trace", iter);
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
                 const ShadeKernel kshade = direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
                 hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out,
                                    counts + 2, pq_out, counts + 3, w.stats.p);
                 HIPCHK(hipGetLastError());
+                sync_check("k_shade", iter);
                 HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 nrays = host_counts[0];
@@ -905,6 +929,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                                    dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
                                    d_accum);
                 HIPCHK(hipGetLastError());
+                sync_check("k_film", 0);
             }
             rr.samples += nb;
         }
@@ -928,6 +953,14 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
     if (rr.st.dim_overflow) throw PtError(PT_ERR_UNSUPPORTED, "Halton dimension table exhausted");
+#ifdef PT_GUARDS
+    unsigned int guard = 0;
+    HIPCHK(hipMemcpyFromSymbol(&guard, HIP_SYMBOL(g_pt_guard), sizeof guard));
+    if (guard)
+        throw PtError(PT_ERR_STATE, "PT_GUARDS: index out of range at " +
+                                        std::string(guard / 100000 == 1 ? "devfuncs.h" : "kernels.hip") + ":" +
+                                        std::to_string(guard % 100000));
+#endif
     if (std::getenv("PT_TRACE_DEBUG") && rr.st.lane_iters)
         std::fprintf(stderr, "[pt] trace SIMD utilisation %.3f (%llu steps / %llu lane-iterations)\n",
                      (double)(rr.st.nodes + rr.st.prims) / (double)rr.st.lane_iters,

@@ -18,7 +18,8 @@ from typing import Optional, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libptgpu.so")
+# PT_LIB selects a diagnostic build of the same library (e.g. libptgpu_guard.so)
+LIB_PATH = os.path.join(HERE, os.environ.get("PT_LIB", "libptgpu.so"))
 
 PT_OK = 0
 STATUS_NAMES = {0: "PT_OK", 1: "PT_ERR_INVALID_ARG", 2: "PT_ERR_PARSE", 3: "PT_ERR_UNSUPPORTED",
