@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3
+#define PT_ABI_VERSION 4
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -85,11 +85,14 @@ enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:
 
 enum pt_filter_kind { PT_FILTER_BOX = 0, PT_FILTER_GAUSSIAN = 1 };
 
-enum pt_light_sample_strategy { PT_LIGHTS_UNIFORM = 0, PT_LIGHTS_POWER = 1 };
+enum pt_light_sample_strategy { PT_LIGHTS_UNIFORM = 0, PT_LIGHTS_POWER = 1,
+                                PT_LIGHTS_SPATIAL = 2 /* SpatialLightDistribution, lightdistrib.cpp:80-330 */ };
 
 enum pt_integrator_kind {
     PT_INTEGRATOR_PATH = 0,    /* PathIntegrator            src/integrators/path.cpp */
-    PT_INTEGRATOR_DIRECT = 1   /* DirectLightingIntegrator  src/integrators/directlighting.cpp */
+    PT_INTEGRATOR_DIRECT = 1,  /* DirectLightingIntegrator  src/integrators/directlighting.cpp */
+    PT_INTEGRATOR_HERO_PATH = 2,     /* HeroPathIntegrator (60-bin SampledSpectrum)  src/integrators/hero_path.cpp */
+    PT_INTEGRATOR_HERO_PATH_MIS = 3  /* HeroPathMISIntegrator                        src/integrators/hero_path_mis.cpp */
 };
 enum pt_direct_strategy {      /* LightStrategy  src/integrators/directlighting.h */
     PT_DIRECT_ALL = 0,         /* "all": UniformSampleAllLights with per-light sample arrays */
@@ -248,6 +251,12 @@ typedef struct pt_scene_desc {
     pt_integrator_desc integrator;
     int32_t n_spheres;
     const pt_sphere* spheres;
+    /* SampledSpectrum scenes (spectral = 1: the hero integrators, which the
+     * reference runs in its PBRT_SAMPLED_SPECTRUM build; 60 bins over
+     * 400-700 nm, spectrum.h:48-51).  NULL / 0 for RGB scenes. */
+    int32_t spectral;
+    const float* material_s60; /* n_materials x 3 x 60: matte Kd | -, glass / dispersive_glass -, Kr, Kt; mirror -, Kr */
+    const float* light_s60;    /* n_lights x 60: area lights' Lemit = L * scale (infinite lights use their RGB L) */
 } pt_scene_desc;
 
 /* ---- statistics (reference counters, src/core/scene.cpp:40-42 etc.) ---- */

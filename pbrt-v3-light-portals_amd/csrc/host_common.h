@@ -101,7 +101,20 @@ void xyz_to_rgb(const float xyz[3], float rgb[3]);
 void rgb_from_sampled(const float* lambda, const float* v, int n, float rgb[3]);
 void rgb_from_blackbody(float T, float scale, float rgb[3]);
 void blackbody_radiance(const float* lambda, int n, float T, float* Le);
-void copper_spectrum(bool k, float rgb[3]);  // metal's default eta (k=false) / k
+void copper_spectrum(bool k, float rgb[3]);
+// 60-bin SampledSpectrum (hero integrators): bins over [400, 700] nm
+constexpr int kNSpec = 60, kLambdaStart = 400, kLambdaEnd = 700;  // spectrum.h:48-51
+struct SpecTables60 {
+    float X[60], Y[60], Z[60];
+    float refl[7][60], illum[7][60];  // White Cyan Magenta Yellow Red Green Blue
+};
+const SpecTables60& spectral_tables();
+float average_spectrum_samples(const float* lambda, const float* vals, int n, float l0, float l1);
+void s60_from_sampled(const float* lambda, const float* v, int n, float out[60]);
+void s60_from_rgb(const float rgb[3], bool reflectance, float out[60]);
+void s60_to_xyz(const float s[60], float xyz[3]);
+float s60_y(const float s[60]);
+void s60_blackbody(float T, float scale, float out[60]);  // metal's default eta (k=false) / k
 bool read_float_file(const std::string& path, std::vector<float>* values);
 // Shape "loopsubdiv" (shapes/loopsubdiv.cpp:137-398): refined limit-surface
 // mesh in object space -- positions, shading normals, triangle indices.

@@ -64,7 +64,8 @@ __device__ __forceinline__ void flush_stats(DevStats* s, unsigned long long cl, 
 template <bool kAny, bool kSph = true>
 __device__ __forceinline__ int traverse(const DevScene& sc, const float4* __restrict__ bnodes,
                                         const float4* __restrict__ bprims, Ray ray, int (*stk)[kTraceBlock],
-                                        int* spill, unsigned long long* nodes, unsigned long long* prims) {
+                                        int* spill, unsigned long long* nodes, unsigned long long* prims,
+                                        float* tOut = nullptr) {
     const int tid = threadIdx.x;
     const V3 inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
     const bool n0 = inv.x < 0, n1 = inv.y < 0, n2 = inv.z < 0;
@@ -142,6 +143,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const float4* __rest
             cur = toVisit < kStackLds ? stk[toVisit][tid] : spill[toVisit - kStackLds];
         }
     }
+    if (tOut) *tOut = ray.tmax;  // GeometricPrimitive::Intersect sets ray.tMax = tHit
     return hitPrim;
 }
 

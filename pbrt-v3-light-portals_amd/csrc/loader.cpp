@@ -274,6 +274,7 @@ struct Param {
     std::string type, name;
     std::vector<double> nums;
     std::vector<std::string> strs;
+    std::vector<float> s60;  // "spectrum"/"blackbody"/"xyz": the SampledSpectrum value (60 bins each)
 };
 
 struct ParamSet {
@@ -319,6 +320,24 @@ struct ParamSet {
         if (!p || p->nums.size() < 3) return false;
         *out = v3((float)p->nums[0], (float)p->nums[1], (float)p->nums[2]);
         return true;
+    }
+    // FindOneSpectrum for the SampledSpectrum build: "rgb" parameters go
+    // through FromRGB with the Illuminant default (paramset.cpp:110-120,
+    // spectrum.h:420-421); spectral ones keep the 60-bin value computed
+    // when the parameter list was parsed.
+    bool spectrum60(const char* n, float out[60]) const {
+        for (auto it = params.rbegin(); it != params.rend(); ++it) {
+            if (it->name != n || it->type != "rgb") continue;
+            if (!it->s60.empty()) {
+                for (int i = 0; i < 60; ++i) out[i] = it->s60[i];
+            } else {
+                if (it->nums.size() < 3) throw PtError(PT_ERR_PARSE, "rgb needs 3 values");
+                const float rgb[3] = {(float)it->nums[0], (float)it->nums[1], (float)it->nums[2]};
+                s60_from_rgb(rgb, false, out);
+            }
+            return true;
+        }
+        return false;
     }
     // FindOneSpectrum for the RGB build: "rgb"/"color" are RGB triples
     // (RGBSpectrum::FromRGB); spectral types were reduced to "rgb" by
@@ -373,6 +392,8 @@ struct pt_host_scene_impl {
     std::vector<pt_light> lights;
     std::vector<pt_portal> portals;
     std::string film_filename = "pbrt.exr";
+    bool spectral = false;
+    std::vector<float> mat_s60, light_s60;  // 3 x 60 per material, 60 per light (spectral scenes)
     pt_scene_desc desc{};
 };
 
@@ -461,13 +482,14 @@ class Loader {
     // "xyz" triples (FromXYZ).  Rewrite them as "rgb" parameters.
     void spectral_to_rgb(Param* p) const {
         std::vector<double> rgbs;
+        std::vector<float> s60;
         auto push = [&](const float c[3]) { for (int k = 0; k < 3; ++k) rgbs.push_back(c[k]); };
         if (p->type == "spectrum") {
             if (!p->strs.empty()) {
                 for (const std::string& name : p->strs) {
                     std::string fn = (!name.empty() && name[0] == '/') ? name : searchDir_ + name;
                     std::vector<float> vals;
-                    float c[3] = {0, 0, 0};
+                    float c[3] = {0, 0, 0}, c60[60] = {0};
                     if (!read_float_file(fn, &vals)) {
                         std::fprintf(stderr, "Warning: Unable to read SPD file \"%s\".  Using black distribution.\n",
                                      fn.c_str());
@@ -475,37 +497,46 @@ class Loader {
                         std::vector<float> wl, v;
                         for (size_t j = 0; j + 1 < vals.size(); j += 2) wl.push_back(vals[j]), v.push_back(vals[j + 1]);
                         rgb_from_sampled(wl.data(), v.data(), (int)wl.size(), c);
+                        s60_from_sampled(wl.data(), v.data(), (int)wl.size(), c60);
                     }
                     push(c);
+                    s60.insert(s60.end(), c60, c60 + 60);
                 }
             } else {
                 if (p->nums.size() % 2) throw PtError(PT_ERR_PARSE, "spectrum \"" + p->name + "\" needs wavelength/value pairs");
                 std::vector<float> wl, v;
                 for (size_t j = 0; j < p->nums.size(); j += 2) wl.push_back((float)p->nums[j]), v.push_back((float)p->nums[j + 1]);
-                float c[3];
+                float c[3], c60[60];
                 rgb_from_sampled(wl.data(), v.data(), (int)wl.size(), c);
+                s60_from_sampled(wl.data(), v.data(), (int)wl.size(), c60);
                 push(c);
+                s60.insert(s60.end(), c60, c60 + 60);
             }
         } else if (p->type == "blackbody") {
             if (p->nums.size() % 2) throw PtError(PT_ERR_PARSE, "blackbody \"" + p->name + "\" needs (T, scale) pairs");
             for (size_t j = 0; j < p->nums.size(); j += 2) {
-                float c[3];
+                float c[3], c60[60];
                 rgb_from_blackbody((float)p->nums[j], (float)p->nums[j + 1], c);
+                s60_blackbody((float)p->nums[j], (float)p->nums[j + 1], c60);
                 push(c);
+                s60.insert(s60.end(), c60, c60 + 60);
             }
         } else if (p->type == "xyz") {
             if (p->nums.size() % 3) throw PtError(PT_ERR_PARSE, "xyz \"" + p->name + "\" needs triples");
             for (size_t j = 0; j < p->nums.size(); j += 3) {
                 const float xyz[3] = {(float)p->nums[j], (float)p->nums[j + 1], (float)p->nums[j + 2]};
-                float c[3];
+                float c[3], c60[60];
                 xyz_to_rgb(xyz, c);
+                s60_from_rgb(c, true, c60);  // FromXYZ: Reflectance default (spectrum.h:422-427)
                 push(c);
+                s60.insert(s60.end(), c60, c60 + 60);
             }
         } else {
             return;
         }
         p->type = "rgb";
         p->nums = std::move(rgbs);
+        p->s60 = std::move(s60);
         p->strs.clear();
     }
 
@@ -595,6 +626,8 @@ class Loader {
                 std::string n = read_string(tk); params(&sampler_, n);
             } else if (d == "Integrator") {
                 std::string n = read_string(tk); params(&integrator_, n);
+                // the hero integrators exist only in the SampledSpectrum build
+                out_->spectral = (n == "hero_path" || n == "hero_path_mis");
             } else if (d == "PixelFilter") {
                 std::string n = read_string(tk); params(&filter_, n);
             } else if (d == "Accelerator") {
@@ -740,6 +773,12 @@ class Loader {
             bool remap = gs_.materialParams.bool1("remaproughness", false);
             remap = shapeParams.bool1("remaproughness", remap);
             m.specular = (ur == 0 && vr == 0) ? 1 : 0;
+            // DispersiveGlassMaterial remaps the shared roughness once per
+            // wavelength BSDF, cumulatively (dispersive_glass.cpp:91-95), so
+            // its four lobes carry four different alphas: not represented.
+            if (disp && remap && !m.specular)
+                throw PtError(PT_ERR_UNSUPPORTED,
+                              "rough dispersive_glass with remaproughness is outside the supported subset");
             if (remap) {
                 ur = tr_roughness_to_alpha(ur);
                 vr = tr_roughness_to_alpha(vr);
@@ -770,8 +809,42 @@ class Loader {
         } else {
             throw PtError(PT_ERR_UNSUPPORTED, "material \"" + name + "\" is outside the supported subset");
         }
+        if (out_->spectral) material_s60(name, shapeParams);
         out_->materials.push_back(m);
         return (int)out_->materials.size() - 1;
+    }
+
+    // 60-bin reflectances of a material in a SampledSpectrum scene, with the
+    // same parameter precedence and defaults as the RGB values above.
+    void material_s60(const std::string& name, const ParamSet& shapeParams) {
+        float v[3][60];
+        auto fill = [&](int slot, const char* pname, float def) {
+            for (int i = 0; i < 60; ++i) v[slot][i] = def;  // Spectrum(def)
+            gs_.materialParams.spectrum60(pname, v[slot]);
+            shapeParams.spectrum60(pname, v[slot]);
+        };
+        for (int k = 0; k < 3; ++k) for (int i = 0; i < 60; ++i) v[k][i] = 0.f;
+        if (name == "matte") fill(0, "Kd", 0.5f);
+        else if (name == "glass" || name == "dispersive_glass") { fill(1, "Kr", 1.f); fill(2, "Kt", 1.f); }
+        else if (name == "mirror") fill(1, "Kr", 0.9f);
+        else if (name != "" && name != "none")
+            throw PtError(PT_ERR_UNSUPPORTED, "material \"" + name + "\" in a SampledSpectrum (hero) scene");
+        for (int k = 0; k < 3; ++k) out_->mat_s60.insert(out_->mat_s60.end(), v[k], v[k] + 60);
+    }
+    void light_s60(const ParamSet& ps, const char* lname, pt_light* L) {
+        float Lv[60], sc[60], out[60];
+        for (int i = 0; i < 60; ++i) Lv[i] = sc[i] = 1.f;  // Spectrum(1.0) defaults
+        ps.spectrum60(lname, Lv);
+        ps.spectrum60("scale", sc);
+        for (int i = 0; i < 60; ++i) out[i] = Lv[i] * sc[i];
+        if (L->kind == PT_LIGHT_INFINITE) {
+            // InfiniteAreaLight keeps an RGB map: texel = (L * scale).ToRGBSpectrum() (infinite.cpp:57-61)
+            float xyz[3];
+            s60_to_xyz(out, xyz);
+            xyz_to_rgb(xyz, L->L);
+            for (int i = 0; i < 60; ++i) out[i] = 0.f;
+        }
+        out_->light_s60.insert(out_->light_s60.end(), out, out + 60);
     }
 
     // CreateTriangleMesh + TriangleMesh ctor (triangle.cpp:55-120): vertices,
@@ -815,6 +888,7 @@ class Loader {
                 pt_light L{};
                 L.kind = PT_LIGHT_DIFFUSE_AREA;
                 diffuse_params(gs_.areaLightParams, &L);
+                if (out_->spectral) light_s60(gs_.areaLightParams, "L", &L);
                 L.shape = ti;
                 L.first_portal = 0; L.n_portals = 0;
                 out_->lights.push_back(L);
@@ -903,6 +977,7 @@ class Loader {
                 pt_light L{};
                 L.kind = PT_LIGHT_DIFFUSE_SPHERE;
                 diffuse_params(gs_.areaLightParams, &L);
+                if (out_->spectral) light_s60(gs_.areaLightParams, "L", &L);
                 L.shape = sidx;
                 out_->lights.push_back(L);
                 sp.area_light = (int)out_->lights.size() - 1;
@@ -927,6 +1002,8 @@ class Loader {
             if (!gs_.areaLight.empty()) {
                 pt_light L{};
                 if (gs_.areaLight == "portal") {
+                    if (out_->spectral)
+                        throw PtError(PT_ERR_UNSUPPORTED, "portal lights in a SampledSpectrum (hero) scene");
                     L.kind = PT_LIGHT_PORTAL_AREA;
                     portal_params(gs_.areaLightParams, &L);
                 } else if (gs_.areaLight == "diffuse" || gs_.areaLight == "area") {
@@ -961,9 +1038,12 @@ class Loader {
             L.n_samples = std::max(1, ps.int1("samples", ps.int1("nsamples", 1)));
             L.shape = -1;
             store_xf(ctm_, &L.light_to_world);
+            if (out_->spectral) light_s60(ps, "L", &L);
             out_->lights.push_back(L);
             return;
         }
+        if (out_->spectral)
+            throw PtError(PT_ERR_UNSUPPORTED, "LightSource \"" + name + "\" in a SampledSpectrum (hero) scene");
         if (name == "point") {
             // CreatePointLight (point.cpp:80-88)
             pt_light L{};
@@ -1131,6 +1211,11 @@ class Loader {
             d.integrator.kind = PT_INTEGRATOR_PATH;
             noRR = true;
             lsDefault = "spatial";
+        } else if (integrator_.name == "hero_path") {
+            d.integrator.kind = PT_INTEGRATOR_HERO_PATH;  // CreateHeroPathIntegrator (hero_path.cpp:192-212)
+        } else if (integrator_.name == "hero_path_mis") {
+            d.integrator.kind = PT_INTEGRATOR_HERO_PATH_MIS;  // CreateHeroPathMISIntegrator (hero_path_mis.cpp:330-354)
+            lsDefault = "spatial";
         } else if (integrator_.name == "directlighting") {
             d.integrator.kind = PT_INTEGRATOR_DIRECT;
             const std::string st = integrator_.ps.string1("strategy", "all");
@@ -1151,7 +1236,12 @@ class Loader {
         std::string ls = integrator_.ps.string1("lightsamplestrategy", lsDefault);
         if (ls == "uniform" || out_->lights.size() == 1) d.integrator.light_strategy = PT_LIGHTS_UNIFORM;
         else if (ls == "power") d.integrator.light_strategy = PT_LIGHTS_POWER;
-        else throw PtError(PT_ERR_UNSUPPORTED, "lightsamplestrategy \"" + ls + "\" with several lights");
+        else if (d.integrator.kind == PT_INTEGRATOR_HERO_PATH_MIS) {
+            if (ls != "spatial")  // unknown names fall back to spatial (lightdistrib.cpp:59-64)
+                std::fprintf(stderr, "Error: Light sample distribution type \"%s\" unknown. Using \"spatial\".\n",
+                             ls.c_str());
+            d.integrator.light_strategy = PT_LIGHTS_SPATIAL;
+        } else throw PtError(PT_ERR_UNSUPPORTED, "lightsamplestrategy \"" + ls + "\" with several lights");
         if (const Param* pb = integrator_.ps.find("pixelbounds", {"integer"})) {
             if (pb->nums.size() == 4) {
                 d.integrator.has_pixel_bounds = 1;
@@ -1184,6 +1274,9 @@ void host_scene_fill_desc(pt_host_scene_impl* hs) {
     d.portals = hs->portals.data();
     d.n_spheres = (int)hs->spheres.size();
     d.spheres = hs->spheres.data();
+    d.spectral = hs->spectral ? 1 : 0;
+    d.material_s60 = hs->spectral ? hs->mat_s60.data() : nullptr;
+    d.light_s60 = hs->spectral ? hs->light_s60.data() : nullptr;
 }
 
 pt_host_scene_impl* load_pbrt_file(const char* path) {

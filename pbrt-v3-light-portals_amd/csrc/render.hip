@@ -16,6 +16,7 @@
 
 #include "host_common.h"
 #include "kernels.hip"
+#include "hero.hip"
 
 namespace pt {
 
@@ -196,6 +197,10 @@ struct pt_scene {
     pt::DBuf<int> psums;
     pt::DBuf<pt::DivMagic> divs;
     pt::DevScene dev{};
+    // hero integrators (SampledSpectrum scenes): tables, light distributions, per-slot radiance
+    bool hero = false;
+    pt::DevHero hh{};
+    pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist, h_out60;
     pt::HaltonPixelConsts hpc{};
     pt::FilmConsts film{};
     pt::Frame fr{};
@@ -322,6 +327,137 @@ static void init_infinite(const pt_light& l, const std::vector<LinearNode>& node
         dl->mfunc[v] = dl->cint[v];
     }
     build1d(dl->mfunc, height, dl->mcdf, &dl->mint);
+}
+
+// RadicalInverse(baseIndex, a) (lowdiscrepancy.cpp:427-...) for the
+// SpatialLightDistribution sample points: base 2 through ReverseBits64 in
+// double, bases 3..11 by RadicalInverseSpecialized (lowdiscrepancy.h:98-111).
+static float radical_inverse_host(int baseIndex, uint64_t a) {
+    if (baseIndex == 0) {
+        uint64_t r = 0;
+        for (int i = 0; i < 64; ++i) r |= ((a >> i) & 1ull) << (63 - i);
+        return (float)(r * 0x1p-64);
+    }
+    static const int primes[5] = {2, 3, 5, 7, 11};
+    const uint64_t base = (uint64_t)primes[baseIndex];
+    const float invBase = (float)1 / (float)base;
+    uint64_t reversed = 0;
+    float invBaseN = 1;
+    while (a) {
+        uint64_t next = a / base, digit = a - next * base;
+        reversed = reversed * base + digit;
+        invBaseN *= invBase;
+        a = next;
+    }
+    return std::min(reversed * invBaseN, 0x1.fffffep-1f);
+}
+// Distribution1D ctor (sampling.h:65-88) into [func | cdf | funcInt]
+static void dist1d_host(const std::vector<float>& f, float* out) {
+    const int n = (int)f.size();
+    for (int i = 0; i < n; ++i) out[i] = f[i];
+    float* cdf = out + n;
+    cdf[0] = 0;
+    for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + f[i - 1] / n;
+    const float funcInt = cdf[n];
+    if (funcInt == 0)
+        for (int i = 1; i < n + 1; ++i) cdf[i] = (float)i / (float)n;
+    else
+        for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+    out[2 * n + 1] = funcInt;
+}
+// HeroSamplerIntegrator::Preprocess (hero.cpp:57-66), HeroPathMIS::Preprocess
+// (hero_path_mis.cpp:104-108): spectral distribution of the summed light
+// power (Light::Power, diffuse.cpp:65-67, infinite.cpp:86-90) and the light
+// sample distribution (lightdistrib.cpp:46-66).
+static void build_hero(pt_scene* s, const pt_scene_desc* d, const std::vector<DevLight>& lights,
+                       const std::vector<float>& area, const std::vector<DevSphere>& spheres) {
+    if (!d->material_s60 || !d->light_s60) throw PtError(PT_ERR_INVALID_ARG, "spectral scene without 60-bin tables");
+    for (int i = 0; i < d->n_lights; ++i)
+        if (d->lights[i].kind == PT_LIGHT_PORTAL_AREA || d->lights[i].kind == PT_LIGHT_POINT)
+            throw PtError(PT_ERR_UNSUPPORTED, "hero integrators support area and infinite lights");
+    const SpecTables60& t = spectral_tables();
+    std::vector<float> xyz(3 * kNSpec), illum(7 * kNSpec);
+    for (int i = 0; i < kNSpec; ++i) { xyz[i] = t.X[i]; xyz[kNSpec + i] = t.Y[i]; xyz[2 * kNSpec + i] = t.Z[i]; }
+    for (int k = 0; k < 7; ++k)
+        for (int i = 0; i < kNSpec; ++i) illum[k * kNSpec + i] = t.illum[k][i];
+    s->h_xyz.upload(xyz);
+    s->h_illum.upload(illum);
+    s->h_mat.upload(d->material_s60, (size_t)d->n_materials * 3 * kNSpec);
+    s->h_light.upload(d->light_s60, (size_t)std::max(1, d->n_lights) * kNSpec);
+    const int nl = d->n_lights;
+    std::vector<std::vector<float>> power((size_t)nl, std::vector<float>(kNSpec));
+    for (int li = 0; li < nl; ++li) {
+        const pt_light& l = d->lights[li];
+        if (l.kind == PT_LIGHT_INFINITE) {
+            const S3 texel = lmap_triangle(lights[li].L, .5f, .5f);  // Lmap->Lookup((.5, .5), .5)
+            float sp[60];
+            s60_from_rgb(texel.c, false, sp);
+            const float k = kPi * lights[li].radius * lights[li].radius;
+            for (int i = 0; i < kNSpec; ++i) power[li][i] = sp[i] * k;
+        } else {
+            const float a = l.kind == PT_LIGHT_DIFFUSE_AREA ? area[l.shape] : spheres[l.shape].area;
+            const float* L = d->light_s60 + (size_t)li * kNSpec;
+            for (int i = 0; i < kNSpec; ++i) power[li][i] = ((L[i] * (float)(l.two_sided ? 2 : 1)) * a) * kPi;
+        }
+    }
+    std::vector<float> sum(kNSpec, 0.f), wcdf(kNSpec + 1);
+    for (int li = 0; li < nl; ++li)
+        for (int i = 0; i < kNSpec; ++i) sum[i] += power[li][i];
+    wcdf[0] = 0.f;  // DiscreteDistribution::Set (distr.h:30-39)
+    for (int i = 0; i < kNSpec; ++i) wcdf[i + 1] = wcdf[i] + sum[i];
+    const float invsum = 1.f / wcdf[kNSpec];
+    for (int i = 1; i < kNSpec; ++i) wcdf[i] *= invsum;
+    wcdf[kNSpec] = 1.0f;
+    s->h_wcdf.upload(wcdf);
+    DevHero& h = s->hh;
+    h = DevHero{};
+    h.XYZ = s->h_xyz.p;
+    h.illum = s->h_illum.p;
+    h.mat_s60 = s->h_mat.p;
+    h.light_s60 = s->h_light.p;
+    h.wcdf = s->h_wcdf.p;
+    h.mis = d->integrator.kind == PT_INTEGRATOR_HERO_PATH_MIS;
+    h.dist_stride = 2 * nl + 2;
+    h.spatial = h.mis && nl > 1 && d->integrator.light_strategy == PT_LIGHTS_SPATIAL;
+    if (!h.spatial) {
+        std::vector<float> func((size_t)std::max(nl, 1), 1.f), dist((size_t)h.dist_stride, 0.f);
+        if (d->integrator.light_strategy == PT_LIGHTS_POWER && nl > 1)
+            for (int li = 0; li < nl; ++li) func[li] = s60_y(power[li].data());
+        if (nl > 0) {
+            func.resize((size_t)nl);
+            dist1d_host(func, dist.data());
+        }
+        s->h_dist.upload(dist);
+    } else {
+        // SpatialLightDistribution ctor (lightdistrib.cpp:80-104): voxel grid over WorldBound()
+        const LinearNode& root = s->host_nodes[0];
+        const V3 mn = v3(root.bmin[0], root.bmin[1], root.bmin[2]), mx = v3(root.bmax[0], root.bmax[1], root.bmax[2]);
+        const V3 diag = mx - mn;
+        const int ax = (diag.x > diag.y && diag.x > diag.z) ? 0 : (diag.y > diag.z ? 1 : 2);
+        const float bmax = diag[ax];
+        int nv[3];
+        for (int i = 0; i < 3; ++i) nv[i] = std::max(1, (int)std::round(diag[i] / bmax * 64));
+        h.nv0 = nv[0]; h.nv1 = nv[1]; h.nv2 = nv[2];
+        h.wb_min = mn; h.wb_max = mx;
+        const size_t nvox = (size_t)nv[0] * nv[1] * nv[2];
+        if (nvox * (size_t)h.dist_stride > ((size_t)1 << 30))
+            throw PtError(PT_ERR_UNSUPPORTED, "spatial light distribution too large (voxels x lights)");
+        s->h_dist.alloc(nvox * (size_t)h.dist_stride);
+        std::vector<float> ri(5 * 128), ly((size_t)nl);
+        for (int i = 0; i < 128; ++i)
+            for (int b = 0; b < 5; ++b) ri[5 * i + b] = radical_inverse_host(b, (uint64_t)i);
+        for (int li = 0; li < nl; ++li) ly[li] = s60_y(d->light_s60 + (size_t)li * kNSpec);
+        DBuf<float> dri, dly;
+        dri.upload(ri);
+        dly.upload(ly);
+        h.dist = s->h_dist.p;
+        hipLaunchKernelGGL(k_hero_spatial, dim3(ceil_div((long)nvox, 128)), dim3(128), 0, 0, s->dev, h, dri.p, dly.p,
+                           s->h_dist.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipDeviceSynchronize());
+    }
+    h.dist = s->h_dist.p;
+    s->hero = true;
 }
 
 static void build_scene(pt_scene* s, const pt_scene_desc* d) {
@@ -723,6 +859,10 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         for (int i = 0; i < d->n_lights; ++i) s->dl_max_samples = std::max(s->dl_max_samples, d->lights[i].n_samples);
     }
     ds.wvl_dim = ds.dl_arrays > 0 ? 5 + 2 * ds.dl_arrays : 5;
+    if (d->spectral && (d->integrator.kind == PT_INTEGRATOR_HERO_PATH || d->integrator.kind == PT_INTEGRATOR_HERO_PATH_MIS))
+        build_hero(s, d, lights, area, spheres);
+    else if (d->integrator.kind == PT_INTEGRATOR_HERO_PATH || d->integrator.kind == PT_INTEGRATOR_HERO_PATH_MIS)
+        throw PtError(PT_ERR_INVALID_ARG, "hero integrators need a spectral (SampledSpectrum) scene description");
 }
 
 // Pixels of tiles t with t % stride == offset, tile order then scan order
@@ -837,6 +977,10 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
              direct ? s->dev.dl_frames : 0);
     HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
     DevPaths ps = w.paths((int)max_slots);
+    if (s->hero) {
+        s->h_out60.alloc(max_slots * (size_t)kNSpec);
+        s->hh.out60 = s->h_out60.p;
+    }
     hipEvent_t ev0, ev1;
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
@@ -869,6 +1013,24 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         for (int s0 = s_begin; s0 < s_end; s0 += g.S) {
             const int ns = std::min(g.S, s_end - s0);
             const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
+            if (s->hero) {
+                // hero integrators: one megakernel pass per batch, then the 60-bin film
+                hipLaunchKernelGGL(k_hero, dim3(std::max(1, std::min(ceil_div(nb, kTraceBlock), maxBlocksTrace))),
+                                   dim3(kTraceBlock), 0, stream, s->dev, s->hh, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc,
+                                   w.spill.p, w.stats.p);
+                HIPCHK(hipGetLastError());
+                sync_check("k_hero", 0);
+                const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
+                if (bw > 0 && bh > 0) {
+                    hipLaunchKernelGGL(k_film_s60, dim3(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32))),
+                                       dim3(256), 0, stream, s->hh, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0,
+                                       bw, bh, d_accum);
+                    HIPCHK(hipGetLastError());
+                    sync_check("k_film_s60", 0);
+                }
+                rr.samples += nb;
+                continue;
+            }
             hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
                                stream, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
             hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);

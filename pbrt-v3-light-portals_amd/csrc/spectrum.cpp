@@ -1,4 +1,7 @@
-// spectrum.cpp -- spectral scene parameters for the RGB build.
+// spectrum.cpp -- spectral scene parameters: reduction to RGB for the RGB
+// build, and the 60-bin SampledSpectrum representation (400-700 nm) the
+// hero-wavelength integrators run in (PBRT_SAMPLED_SPECTRUM build,
+// spectrum.h:304-440, spectrum.cpp:59-178).
 //
 // pbrt-v3 is built with Spectrum = RGBSpectrum (`PBRT_SAMPLED_SPECTRUM` off,
 // reference src/core/pbrt.h), so every "spectrum" / "blackbody" / "xyz"
@@ -16,6 +19,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cmath>
+#include <limits>
 #include <cstdlib>
 #include <cstdio>
 #include <string>
@@ -28,6 +32,7 @@
 namespace pt {
 
 static const int kNCIE = 471;
+static const float kInfF = std::numeric_limits<float>::infinity();
 static const float kCIE_Y_integral = 106.856895f;  // spectrum.h:83
 
 static float lerpf(float t, float a, float b) { return (1 - t) * a + t * b; }  // pbrt.h:422
@@ -110,6 +115,138 @@ void rgb_from_blackbody(float T, float scale, float rgb[3]) {  // paramset.cpp:1
     float s[3];
     rgb_from_sampled(kCIE_lambda, v.data(), kNCIE, s);
     for (int k = 0; k < 3; ++k) rgb[k] = scale * s[k];
+}
+
+// ---------------------------------------------------------------------------
+// SampledSpectrum (60 bins over [400, 700] nm)
+// ---------------------------------------------------------------------------
+// AverageSpectrumSamples (spectrum.cpp:59-90): the segment sums are formed in
+// double (`0.5 * (...)` promotes) and narrowed to float on each +=.
+float average_spectrum_samples(const float* lambda, const float* vals, int n, float l0, float l1) {
+    if (l1 <= lambda[0]) return vals[0];
+    if (l0 >= lambda[n - 1]) return vals[n - 1];
+    if (n == 1) return vals[0];
+    float sum = 0;
+    if (l0 < lambda[0]) sum += vals[0] * (lambda[0] - l0);
+    if (l1 > lambda[n - 1]) sum += vals[n - 1] * (l1 - lambda[n - 1]);
+    int i = 0;
+    while (l0 > lambda[i + 1]) ++i;
+    auto interp = [&](float w, int k) { return lerpf((w - lambda[k]) / (lambda[k + 1] - lambda[k]), vals[k], vals[k + 1]); };
+    for (; i + 1 < n && l1 >= lambda[i]; ++i) {
+        const float a = std::max(l0, lambda[i]), b = std::min(l1, lambda[i + 1]);
+        sum = (float)((double)sum + 0.5 * (double)(interp(a, i) + interp(b, i)) * (double)(b - a));
+    }
+    return sum / (l1 - l0);
+}
+
+static void bin_range(int i, float* l0, float* l1) {  // Lerp(Float(i) / Float(60), 400, 700)
+    *l0 = lerpf(float(i) / float(kNSpec), (float)kLambdaStart, (float)kLambdaEnd);
+    *l1 = lerpf(float(i + 1) / float(kNSpec), (float)kLambdaStart, (float)kLambdaEnd);
+}
+
+const SpecTables60& spectral_tables() {  // SampledSpectrum::Init (spectrum.h:330-393)
+    static SpecTables60 t;
+    static bool init = false;
+    if (!init) {
+        const float* refl[7] = {kRGBRefl2SpectWhite, kRGBRefl2SpectCyan, kRGBRefl2SpectMagenta, kRGBRefl2SpectYellow,
+                                kRGBRefl2SpectRed, kRGBRefl2SpectGreen, kRGBRefl2SpectBlue};
+        const float* illum[7] = {kRGBIllum2SpectWhite, kRGBIllum2SpectCyan, kRGBIllum2SpectMagenta,
+                                 kRGBIllum2SpectYellow, kRGBIllum2SpectRed, kRGBIllum2SpectGreen, kRGBIllum2SpectBlue};
+        for (int i = 0; i < kNSpec; ++i) {
+            float l0, l1;
+            bin_range(i, &l0, &l1);
+            t.X[i] = average_spectrum_samples(kCIE_lambda, kCIE_X, kNCIE, l0, l1);
+            t.Y[i] = average_spectrum_samples(kCIE_lambda, kCIE_Y, kNCIE, l0, l1);
+            t.Z[i] = average_spectrum_samples(kCIE_lambda, kCIE_Z, kNCIE, l0, l1);
+            for (int k = 0; k < 7; ++k) {
+                t.refl[k][i] = average_spectrum_samples(kRGB2SpectLambda, refl[k], 32, l0, l1);
+                t.illum[k][i] = average_spectrum_samples(kRGB2SpectLambda, illum[k], 32, l0, l1);
+            }
+        }
+        init = true;
+    }
+    return t;
+}
+
+void s60_from_sampled(const float* lambda_in, const float* v_in, int n, float out[60]) {  // spectrum.h:310-328
+    if (n <= 0) throw PtError(PT_ERR_PARSE, "empty spectrum");
+    std::vector<float> lambda(lambda_in, lambda_in + n), v(v_in, v_in + n);
+    bool sorted = true;
+    for (int i = 0; i < n - 1; ++i)
+        if (lambda[i] > lambda[i + 1]) sorted = false;
+    if (!sorted) {
+        std::vector<std::pair<float, float>> sv;
+        for (int i = 0; i < n; ++i) sv.emplace_back(lambda[i], v[i]);
+        std::sort(sv.begin(), sv.end());
+        for (int i = 0; i < n; ++i) lambda[i] = sv[i].first, v[i] = sv[i].second;
+    }
+    for (int i = 0; i < n - 1; ++i)
+        if (!(lambda[i + 1] > lambda[i]))
+            throw PtError(PT_ERR_PARSE, "spectrum wavelengths must be strictly increasing");
+    for (int i = 0; i < kNSpec; ++i) {
+        float l0, l1;
+        bin_range(i, &l0, &l1);
+        out[i] = average_spectrum_samples(lambda.data(), v.data(), n, l0, l1);
+    }
+}
+
+// SampledSpectrum::FromRGB (spectrum.cpp:98-172): Smits' basis, then Clamp().
+void s60_from_rgb(const float rgb[3], bool reflectance, float out[60]) {
+    const SpecTables60& t = spectral_tables();
+    const float(*b)[60] = reflectance ? t.refl : t.illum;  // W C M Y R G B
+    enum { W, C, M, Y, R, G, B };
+    float r[60] = {0};
+    auto add = [&](float a, int k) { for (int i = 0; i < kNSpec; ++i) r[i] += b[k][i] * a; };
+    if (rgb[0] <= rgb[1] && rgb[0] <= rgb[2]) {
+        add(rgb[0], W);
+        if (rgb[1] <= rgb[2]) { add(rgb[1] - rgb[0], C); add(rgb[2] - rgb[1], B); }
+        else { add(rgb[2] - rgb[0], C); add(rgb[1] - rgb[2], G); }
+    } else if (rgb[1] <= rgb[0] && rgb[1] <= rgb[2]) {
+        add(rgb[1], W);
+        if (rgb[0] <= rgb[2]) { add(rgb[0] - rgb[1], M); add(rgb[2] - rgb[0], B); }
+        else { add(rgb[2] - rgb[1], M); add(rgb[0] - rgb[2], R); }
+    } else {
+        add(rgb[2], W);
+        if (rgb[0] <= rgb[1]) { add(rgb[0] - rgb[2], Y); add(rgb[1] - rgb[0], G); }
+        else { add(rgb[1] - rgb[2], Y); add(rgb[0] - rgb[1], R); }
+    }
+    const float sc = reflectance ? (float).94 : .86445f;
+    for (int i = 0; i < kNSpec; ++i) {
+        r[i] *= sc;
+        out[i] = r[i] < 0 ? 0.f : (r[i] > kInfF ? kInfF : r[i]);  // Clamp(0, Infinity)
+    }
+}
+
+void s60_to_xyz(const float s[60], float xyz[3]) {  // SampledSpectrum::ToXYZ (spectrum.h:395-406)
+    const SpecTables60& t = spectral_tables();
+    xyz[0] = xyz[1] = xyz[2] = 0.f;
+    for (int i = 0; i < kNSpec; ++i) {
+        xyz[0] += t.X[i] * s[i];
+        xyz[1] += t.Y[i] * s[i];
+        xyz[2] += t.Z[i] * s[i];
+    }
+    const float scale = float(kLambdaEnd - kLambdaStart) / float(kCIE_Y_integral * kNSpec);
+    xyz[0] *= scale;
+    xyz[1] *= scale;
+    xyz[2] *= scale;
+}
+
+float s60_y(const float s[60]) {  // SampledSpectrum::y (spectrum.h:407-413)
+    const SpecTables60& t = spectral_tables();
+    float yy = 0.f;
+    for (int i = 0; i < kNSpec; ++i) yy += t.Y[i] * s[i];
+    return yy * float(kLambdaEnd - kLambdaStart) / float(kCIE_Y_integral * kNSpec);
+}
+
+void s60_blackbody(float T, float scale, float out[60]) {  // paramset.cpp:134-150, SampledSpectrum build
+    std::vector<float> v(kNCIE);
+    blackbody_radiance(kCIE_lambda, kNCIE, T, v.data());
+    float lambdaMax = 2.8977721e-3 / T * 1e9;
+    float maxL;
+    blackbody_radiance(&lambdaMax, 1, T, &maxL);
+    for (int i = 0; i < kNCIE; ++i) v[i] /= maxL;
+    s60_from_sampled(kCIE_lambda, v.data(), kNCIE, out);
+    for (int i = 0; i < kNSpec; ++i) out[i] = out[i] * scale;
 }
 
 void copper_spectrum(bool k, float rgb[3]) {  // metal.cpp:116-122

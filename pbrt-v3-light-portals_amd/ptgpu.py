@@ -166,7 +166,24 @@ class pt_scene_desc(ctypes.Structure):
         ("n_lights", ctypes.c_int32), ("lights", ctypes.c_void_p), ("n_portals", ctypes.c_int32),
         ("portals", ctypes.c_void_p), ("bvh_max_prims", ctypes.c_int32), ("camera", pt_camera_desc),
         ("film", pt_film_desc), ("sampler", pt_sampler_desc), ("integrator", pt_integrator_desc),
-        ("n_spheres", ctypes.c_int32), ("spheres", ctypes.c_void_p)]
+        ("n_spheres", ctypes.c_int32), ("spheres", ctypes.c_void_p), ("spectral", ctypes.c_int32),
+        ("material_s60", ctypes.POINTER(ctypes.c_float)), ("light_s60", ctypes.POINTER(ctypes.c_float))]
+
+
+def scene_desc(hs: "HostScene") -> pt_scene_desc:
+    """The scene's pt_scene_desc (a view into the loader's memory) -- host only."""
+    return ctypes.cast(ctypes.c_void_p(hs.desc), ctypes.POINTER(pt_scene_desc)).contents
+
+
+def spectral_tables(hs: "HostScene"):
+    """(material_s60 (n_materials, 3, 60), light_s60 (n_lights, 60)) of a
+    SampledSpectrum scene, or None for an RGB scene."""
+    d = scene_desc(hs)
+    if not d.spectral:
+        return None
+    m = np.ctypeslib.as_array(d.material_s60, shape=(d.n_materials, 3, 60)).copy()
+    lt = np.ctypeslib.as_array(d.light_s60, shape=(max(1, d.n_lights), 60)).copy()[:d.n_lights]
+    return m, lt
 
 
 def integrator_desc(hs: "HostScene") -> pt_integrator_desc:
