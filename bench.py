@@ -36,6 +36,8 @@ CONFIGS = {
            "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)"),
     "c3": ("cornell_dielectric.pbrt", "cornell dielectric (config 3)", "path maxdepth 5",
            "reference scenes/cornell_dielectric.pbrt (spectral params reduced to RGB) with Integrator path, 1024 spp"),
+    "c3h": ("cornell_dielectric_hero.pbrt", "cornell dielectric as written (config 3)", "hero_path_mis",
+            "reference scenes/cornell_dielectric.pbrt as written (SampledSpectrum, Integrator hero_path_mis), 1024 spp"),
     "c4": ("portal_room.pbrt", "portal room (config 4)", "path maxdepth 8",
            "synthetic (scenes/portal_room.pbrt from scripts/make_portal_room.py: room + 4 portals + sky; Halton)"),
     "c5": ("killeroo_atrium.pbrt", "killeroo atrium 10M tris (config 5)", "path maxdepth 5",
@@ -211,7 +213,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic, 1) if traffic is not None else None,
                          "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
-                         "kernel": "k_trace", "algorithmic_bytes_per_launch": round(
+                         "kernel": "k_hero" if "hero" in cdepth else "k_trace", "algorithmic_bytes_per_launch": round(
                              alg_bytes / max(1, agg["trace_launches"]), 1),
                          "avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4)},
         }

@@ -1015,9 +1015,13 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
             if (s->hero) {
                 // hero integrators: one megakernel pass per batch, then the 60-bin film
+                auto e = tev_get(tcount++);
+                HIPCHK(hipEventRecord(e.first, stream));
                 hipLaunchKernelGGL(k_hero, dim3(std::max(1, std::min(ceil_div(nb, kTraceBlock), maxBlocksTrace))),
                                    dim3(kTraceBlock), 0, stream, s->dev, s->hh, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc,
                                    w.spill.p, w.stats.p);
+                HIPCHK(hipEventRecord(e.second, stream));
+                rr.launches++;
                 HIPCHK(hipGetLastError());
                 sync_check("k_hero", 0);
                 const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
