@@ -213,7 +213,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic, 1) if traffic is not None else None,
                          "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
-                         "kernel": "k_hero" if "hero" in cdepth else "k_trace", "algorithmic_bytes_per_launch": round(
+                         "kernel": "k_trace", "algorithmic_bytes_per_launch": round(
                              alg_bytes / max(1, agg["trace_launches"]), 1),
                          "avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4)},
         }

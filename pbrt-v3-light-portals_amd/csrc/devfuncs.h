@@ -30,12 +30,29 @@ __device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, i
     const uint16_t* perm = sc.perm + sc.prime_sums[dim];
     uint64_t rev = 0;
     float invBaseN = 1;
+    // Digits four at a time: the digit chain is ALU only, so the four
+    // permutation gathers are issued back to back and waited on once (a
+    // digit past the end is 0, a valid index whose entry is not used).  The
+    // accumulation keeps the reference's per-digit order.
     while (a) {
-        uint32_t next = fast_div(a, dm);
-        uint32_t digit = a - next * dm.base;
-        rev = rev * dm.base + perm[digit];
-        invBaseN *= dm.inv_base;
-        a = next;
+        uint32_t d[4], live = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t next = fast_div(a, dm);
+            d[k] = a - next * dm.base;
+            live += a != 0u ? 1u : 0u;
+            a = next;
+        }
+        uint32_t pv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pv[k] = perm[d[k]];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if ((uint32_t)k < live) {
+                rev = rev * dm.base + pv[k];
+                invBaseN *= dm.inv_base;
+            }
+        }
     }
     return smin(invBaseN * ((float)rev + sc.perm_c0[dim]), kOneMinusEps);
 }
@@ -125,19 +142,34 @@ __device__ __forceinline__ bool tri_test(V3 p0, V3 p1, V3 p2, const Ray& ray, fl
     return true;
 }
 
+// The ray-only part of Triangle::Intersect's set-up (triangle.cpp:205-222):
+// the permutation axis kz and the shear Sx, Sy, Sz, computed once per ray by
+// the traversal kernels instead of once per primitive test (same operations,
+// so the same values).
+struct TriShear {
+    float sx, sy, sz;
+    int kz;
+};
+__device__ __forceinline__ TriShear tri_shear(const V3& rd) {
+    const int kz = maxdim(vabs(rd));
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    const V3 d = permute(rd, kx, ky, kz);
+    return TriShear{-d.x / d.z, -d.y / d.z, 1.f / d.z, kz};
+}
+
 // Accept/reject + t of tri_test, written for SIMD execution: the same float
 // operations in the same order, the early exits folded into one predicate
 // (only the rare double-precision edge recomputation stays a branch).
-__device__ __forceinline__ bool tri_hit(V3 p0, V3 p1, V3 p2, const Ray& ray, float* tHit) {
+__device__ __forceinline__ bool tri_hit(V3 p0, V3 p1, V3 p2, const Ray& ray, const TriShear& sh, float* tHit) {
     V3 p0t = p0 - ray.o, p1t = p1 - ray.o, p2t = p2 - ray.o;
-    const int kz = maxdim(vabs(ray.d));
+    const int kz = sh.kz;
     int kx = kz + 1; if (kx == 3) kx = 0;
     int ky = kx + 1; if (ky == 3) ky = 0;
-    const V3 d = permute(ray.d, kx, ky, kz);
     p0t = permute(p0t, kx, ky, kz);
     p1t = permute(p1t, kx, ky, kz);
     p2t = permute(p2t, kx, ky, kz);
-    const float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1.f / d.z;
+    const float Sx = sh.sx, Sy = sh.sy, Sz = sh.sz;
     p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
     p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
     p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
@@ -884,7 +916,7 @@ __device__ __forceinline__ float bsdf_pdf(const Bsdf& b, V3 woW, V3 wiW, int fla
 // returns black before writing it; *sampled is the sampled BxDFType.
 template <int kFt = kFtAll>
 __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float u0, float u1, float* pdf, int flags,
-                                          int* sampled) {
+                                          int* sampled, V3* wiLocal = nullptr) {
     const int matchingComps = bsdf_num<kFt>(b, flags);
     if (matchingComps == 0) { *pdf = 0; *sampled = 0; return s3(0.f); }
     int comp = (int)floorf(u0 * matchingComps);
@@ -903,6 +935,7 @@ __device__ __forceinline__ S3 bsdf_sample(const Bsdf& b, V3 woW, V3* wiW, float 
     S3 f = lobe_sample<kFt>(b, bk, wo, &wi, ur0, u1, pdf, sampled);
     if (*pdf == 0) { *sampled = 0; return s3(0.f); }
     *wiW = l2w(b, wi);
+    if (wiLocal) *wiLocal = wi;
     const bool spec = (lobe_type(bk) & kBxSpecular) != 0;
     if (!spec && matchingComps > 1)
         for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {

@@ -20,6 +20,19 @@ namespace pt {
 
 constexpr int kNS = 60;
 
+// The 60-bin loops over the bin-major state run in groups of kG bins: a
+// group's loads are all issued before its stores (the arrays may alias, so
+// the compiler cannot move a load above an earlier store itself).
+constexpr int kG = 12;
+__device__ __forceinline__ void gload(const float* g, uint32_t N, int i0, float* r) {
+#pragma unroll
+    for (int j = 0; j < kG; ++j) r[j] = g[(uint32_t)(i0 + j) * N];
+}
+__device__ __forceinline__ void gstore(float* g, uint32_t N, int i0, const float* r) {
+#pragma unroll
+    for (int j = 0; j < kG; ++j) g[(uint32_t)(i0 + j) * N] = r[j];
+}
+
 struct DevHero {
     const float* XYZ;        // 3 x 60 CIE matching functions (SampledSpectrum::Init)
     const float* illum;      // 7 x 60 RGB->illuminant basis (W C M Y R G B)
@@ -120,6 +133,37 @@ __device__ __forceinline__ float hb_f1(const DevHero& h, HeroBsdf* hb, V3 wo, V3
     return bsdf_f<kFtAll>(hb->b, wo, wi, kBxAll).c[bin % 3];
 }
 
+// The lobe sum of BSDF::f (reflection.cpp:713-726) for local directions and
+// a fixed reflect test, at the chunk the material copy currently holds.
+__device__ __forceinline__ S3 hb_lobes_f(const Bsdf& b, V3 wo, V3 wi, bool reflect) {
+    S3 f = s3(0.f);
+    for (int i = 0; i < Ft<kFtAll>::max_lobes; ++i) {
+        if (i >= b.n) break;
+        const int k = lobe_at(b, i), t = lobe_type(k);
+        if (lobe_matches(k, kBxAll) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT))))
+            f = f + lobe_f<kFtAll>(b, k, wo, wi);
+    }
+    return f;
+}
+// BSDF::f over all 60 bins: the shading-frame change and the reflect test
+// once, the lobe values per 3-bin chunk; out(k, f) receives chunk k.
+template <typename Out>
+__device__ __forceinline__ void hb_f_all(const DevHero& h, HeroBsdf* hb, V3 woW, V3 wiW, Out out) {
+    const Bsdf& b = hb->b;
+    const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
+    const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    for (int i0 = 0; i0 < kNS; i0 += kG) {  // out(i0, f) receives bins i0 .. i0 + kG - 1
+        float f[kG];
+#pragma unroll
+        for (int c = 0; c < kG / 3; ++c) {
+            hb_chunk(h, hb, i0 / 3 + c);
+            const S3 v = wo.z == 0 ? s3(0.f) : hb_lobes_f(b, wo, wi, reflect);
+            f[3 * c] = v.c[0]; f[3 * c + 1] = v.c[1]; f[3 * c + 2] = v.c[2];
+        }
+        out(i0, f);
+    }
+}
+
 // light distribution of a point (lightdistrib.cpp:68-78, 112-175)
 __device__ __forceinline__ const float* hero_dist(const DevHero& h, V3 p) {
     if (!h.spatial) return h.dist;
@@ -149,236 +193,56 @@ __device__ __forceinline__ void light_L60(const DevHero& h, const DevLight& l, i
     for (int i = 0; i < kNS; ++i) out[i] = vis ? L[i] : 0.f;
 }
 
-struct HeroCounters {
-    unsigned long long closest, shadow, nodes, prims;
+// Per-slot state of a hero path on the wavefront (bin-major SoA, stride n):
+// the 60-bin throughput, radiance and pending light-sample contribution, and
+// the scalars of hero_path*.cpp's loop.
+struct DevHeroPaths {
+    float* beta;  // 60 n
+    float* L;     // 60 n; copied to DevHero::out60 (slot-major, k_film_s60's layout) when the path ends
+    float* nee;   // 60 n: SampleEmitterHero's term, added if its shadow ray is unoccluded
+    float* hs;    // kHs n
 };
+constexpr int kHsWvl = 0;       // 4: the hero wavelengths
+constexpr int kHsPath = 4;      // 4: pathWvlPdf
+constexpr int kHsPrev = 8;      // 4: prevPathWvlPdf
+constexpr int kHsEtaScale = 12;
+constexpr int kHsBsdfPdf = 13;
+constexpr int kHsFlags = 14;    // kHf* (uint bits)
+constexpr int kHs = 15;
+constexpr uint32_t kHfWvlDep = 1u, kHfLastSpec = 2u, kHfPend = 4u;
 
-// One hero path (hero_path.cpp:57-189, hero_path_mis.cpp:110-327).
-__device__ void hero_li(const DevScene& sc, const DevHero& h, Ray ray, const float* wvls, Dims& dm,
-                        int (*stk)[kTraceBlock], int* spill, HeroCounters& ctr, float* Lo) {
-    float beta[kNS], wvlPdf[kNS], f[kNS], tmp[kNS];
-    for (int i = 0; i < kNS; ++i) { Lo[i] = 0.f; beta[i] = 1.f; wvlPdf[i] = 1.f; }
-    float etaScale = 1, bsdfPdf = 0;
-    bool isWvlDependent = false, isLastSpecular = false;
-    float pathWvlPdf[4] = {1, 1, 1, 1}, prev[4] = {1, 1, 1, 1};
-    int wvlIdx[4];
-    for (int i = 0; i < 4; ++i) {
-        int idx = (int)((wvls[i] - (float)400) * ((float)kNS / (float)300));  // indexFromWavelength
-        wvlIdx[i] = idx < kNS - 1 ? idx : kNS - 1;
-        wvlPdf[wvlIdx[i]] = h.wcdf[wvlIdx[i] + 1] - h.wcdf[wvlIdx[i]];
+
+__device__ __forceinline__ int wvl_index(float w) {  // indexFromWavelength
+    const int idx = (int)((w - (float)400) * ((float)kNS / (float)300));
+    return idx < kNS - 1 ? idx : kNS - 1;
+}
+// wvlPdf[b]: 1, or the SpectralDistribution pdf of the bin for the hero bins
+__device__ __forceinline__ float wvl_pdf(const DevHero& h, const int* wi, int b) {
+    return (wi[0] == b || wi[1] == b || wi[2] == b || wi[3] == b) ? h.wcdf[b + 1] - h.wcdf[b] : 1.f;
+}
+// t of the closest hit found by the traversal (ray.tMax after BVHAccel::Intersect):
+// the hit primitive's own test gives the same t whatever tMax was when it hit
+__device__ __forceinline__ float hit_t(const DevScene& sc, int prim, const Ray& ray) {
+    const float4 r0 = sc.prims[3 * PT_IDX(prim, sc.n_prims)];
+    const float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
+    const uint32_t fl = __float_as_uint(r0.w);
+    float t = kInf;
+    if (fl & kPrimAnalytic) {
+        shape_test<true>(sc, fl, __float_as_int(r1.w), ray, &t);
+    } else {
+        const float4 r2 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 2];
+        tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, tri_shear(ray.d), &t);
     }
-    for (int bounces = 0;; ++bounces) {
-        const V3 rayO = ray.o;
-        float tHit = kInf;
-        ++ctr.closest;
-        const int hp = traverse<false, true>(sc, sc.nodes, sc.prims, ray, stk, spill, &ctr.nodes, &ctr.prims, &tHit);
-        SurfHit si;
-        const bool found = hp >= 0 && surface_at<true>(sc, hp, ray, &si);
-        if (!found) {
-            for (int li = 0; li < sc.n_lights; ++li) {
-                const DevLight& l = sc.lights[li];
-                if (l.kind != PT_LIGHT_INFINITE) continue;
-                s60_from_rgb_illum(h, inf_Le(l, ray.d), tmp);  // Spectrum(Lmap->Lookup, Illuminant)
-                if (s60_black(tmp)) continue;
-                if (!h.mis) {
-                    const float sw = pathWvlPdf[0] + pathWvlPdf[1] + pathWvlPdf[2] + pathWvlPdf[3];
-                    for (int i = 0; i < kNS; ++i)
-                        Lo[i] += isWvlDependent ? (beta[i] * tmp[i]) / (wvlPdf[i] * sw) : beta[i] * tmp[i];
-                } else if (bounces == 0) {
-                    for (int i = 0; i < kNS; ++i) Lo[i] += beta[i] * tmp[i];
-                } else {
-                    const float emPdf = isLastSpecular ? 0.f : inf_pdf_li(l, ray.d);
-                    const float s = (pathWvlPdf[0] + prev[0] * emPdf) + (pathWvlPdf[1] + prev[1] * emPdf) +
-                                    (pathWvlPdf[2] + prev[2] * emPdf) + (pathWvlPdf[3] + prev[3] * emPdf);
-                    const float mwc = bsdfPdf / (bsdfPdf + emPdf);
-                    for (int i = 0; i < kNS; ++i)
-                        Lo[i] += (beta[i] * tmp[i]) * (isWvlDependent ? 1.0f / (wvlPdf[i] * s) : mwc);
-                }
-            }
-            break;
-        }
-        int mat, light;
-        prim_info<true>(sc, hp, &mat, &light);
-        if (light >= 0) {
-            const DevLight& l = sc.lights[PT_IDX(light, sc.n_lights)];
-            light_L60(h, l, light, si.n, -ray.d, tmp);
-            if (!s60_black(tmp)) {
-                if (!h.mis) {
-                    const float sw = pathWvlPdf[0] + pathWvlPdf[1] + pathWvlPdf[2] + pathWvlPdf[3];
-                    for (int i = 0; i < kNS; ++i)
-                        Lo[i] += isWvlDependent ? (beta[i] * tmp[i]) / (wvlPdf[i] * sw) : beta[i] * tmp[i];
-                } else if (bounces == 0) {
-                    for (int i = 0; i < kNS; ++i) Lo[i] += beta[i] * tmp[i];
-                } else {
-                    float emPdf = 0;
-                    if (!isLastSpecular) {  // PdfEmitterHero (hero_path_mis.cpp:46-76)
-                        emPdf = (tHit * tHit) / (absdot(si.n, si.wo) * l.area);  // it.shape->Area()
-                        const float* d = hero_dist(h, rayO);
-                        const int nl = sc.n_lights;
-                        emPdf = emPdf * (d[light] / (d[2 * nl + 1] * nl));
-                    }
-                    const float s = (pathWvlPdf[0] + prev[0] * emPdf) + (pathWvlPdf[1] + prev[1] * emPdf) +
-                                    (pathWvlPdf[2] + prev[2] * emPdf) + (pathWvlPdf[3] + prev[3] * emPdf);
-                    const float mwc = bsdfPdf / (bsdfPdf + emPdf);
-                    for (int i = 0; i < kNS; ++i)
-                        Lo[i] += (beta[i] * tmp[i]) * (isWvlDependent ? 1.0f / (wvlPdf[i] * s) : mwc);
-                }
-            }
-        }
-        if (bounces >= sc.max_depth) break;
-        const pt_material& M = sc.mats[PT_IDX(mat, sc.n_mats)];
-        if (M.kind == PT_MAT_NONE) {
-            ray = Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
-            bounces--;
-            continue;
-        }
-        const bool disp = M.kind == PT_MAT_DISPERSIVE_GLASS;
-        HeroBsdf hb[4];
-        bool isectWvlDep = false;
-        if (disp) {  // one BSDF per wavelength (dispersive_glass.cpp:62-118)
-            const float lminsq = (float)(400 * 400), lmaxsq = (float)(700 * 700);
-            const float cauchyB = (lminsq * M.ior_max - lmaxsq * M.ior_min) / (lminsq - lmaxsq);
-            const float cauchyC = lminsq * (M.ior_max - cauchyB);
-            for (int i = 0; i < 4; ++i) hb_make(sc, h, mat, si, cauchyB + cauchyC / (wvls[i] * wvls[i]), &hb[i]);
-            isectWvlDep = hb[0].b.n > 0;
-        } else {
-            hb_make(sc, h, mat, si, M.ior, &hb[0]);
-        }
-        if (h.mis && bsdf_num<kFtAll>(hb[0].b, kBxNonSpecular) > 0 && sc.n_lights > 0) {
-            // SampleEmitterHero (hero_path_mis.cpp:78-108)
-            const float* d = hero_dist(h, si.p);
-            const int nl = sc.n_lights;
-            float emPdf = 0;
-            V3 wi = v3(0, 0, 0);
-            bool haveLi = false;
-            float lpdf;
-            const int li = dist_sample(d, nl, dm.get1(), &lpdf);
-            emPdf = lpdf;
-            if (lpdf != 0.f) {
-                const float u0 = dm.get1(), u1 = dm.get1();
-                float epdf = 0;
-                V3 sp, sn, spe;
-                const DevLight& l = sc.lights[PT_IDX(li, sc.n_lights)];
-                const S3 Lrgb = area_sample_li<kFtAll>(sc, l, si, u0, u1, &wi, &epdf, &sp, &sn, &spe);
-                bool occluded = true;
-                if (epdf != 0.f) {
-                    const V3 origin = offset_ray_origin(si.p, si.perr, si.n, sp - si.p);
-                    const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
-                    ++ctr.shadow;
-                    occluded = traverse<true, true>(sc, sc.nodes, sc.prims, Ray{origin, target - origin, 1 - kShadowEps},
-                                                    stk, spill, &ctr.nodes, &ctr.prims) >= 0;
-                }
-                if (epdf == 0.f || occluded) emPdf = 0.f;
-                else {
-                    emPdf = emPdf * epdf;
-                    if (l.kind == PT_LIGHT_INFINITE) s60_from_rgb_illum(h, Lrgb, tmp);
-                    else light_L60(h, l, li, sn, -wi, tmp);
-                    for (int i = 0; i < kNS; ++i) tmp[i] = tmp[i] / emPdf;
-                    haveLi = !s60_black(tmp);
-                }
-            }
-            if (haveLi && emPdf > 0.f) {
-                const V3 wo = si.wo;
-                hb_f(h, &hb[0], wo, wi, f);
-                if (!s60_black(f)) {
-                    float mw[kNS];
-                    if (isWvlDependent || isectWvlDep) {
-                        for (int i = 0; i < kNS; ++i) f[i] = 0.0f;
-                        float bp[4];
-                        for (int i = 0; i < 4; ++i) {
-                            HeroBsdf* b = &hb[isectWvlDep ? i : 0];
-                            f[wvlIdx[i]] += hb_f1(h, b, wo, wi, wvlIdx[i]);
-                            bp[i] = bsdf_pdf<kFtAll>(b->b, wo, wi, kBxAll);
-                        }
-                        const float s = (pathWvlPdf[0] * emPdf + pathWvlPdf[0] * bp[0]) +
-                                        (pathWvlPdf[1] * emPdf + pathWvlPdf[1] * bp[1]) +
-                                        (pathWvlPdf[2] * emPdf + pathWvlPdf[2] * bp[2]) +
-                                        (pathWvlPdf[3] * emPdf + pathWvlPdf[3] * bp[3]);
-                        for (int i = 0; i < kNS; ++i) mw[i] = emPdf / (wvlPdf[i] * s);
-                    } else {
-                        const float bp = bsdf_pdf<kFtAll>(hb[0].b, wo, wi, kBxAll);
-                        const float m = emPdf / (emPdf + bp);
-                        for (int i = 0; i < kNS; ++i) mw[i] = m;
-                    }
-                    const float cosv = absdot(wi, si.sn);
-                    for (int i = 0; i < kNS; ++i) f[i] *= cosv;
-                    for (int i = 0; i < kNS; ++i) Lo[i] += ((beta[i] * tmp[i]) * f[i]) * mw[i];
-                }
-            }
-        }
-        // BSDF sampling
-        const V3 wo = -ray.d;
-        V3 wi = v3(0, 0, 0);
-        int flags = 0;
-        const float u0 = dm.get1(), u1 = dm.get1();
-        bsdfPdf = 0;
-        for (int k = 0; k < kNS / 3; ++k) {
-            hb_chunk(h, &hb[0], k);
-            const S3 v = bsdf_sample<kFtAll>(hb[0].b, wo, &wi, u0, u1, &bsdfPdf, kBxAll, &flags);
-            f[3 * k] = v.c[0]; f[3 * k + 1] = v.c[1]; f[3 * k + 2] = v.c[2];
-        }
-        if (s60_black(f) || bsdfPdf == 0.f) break;
-        const bool curWvlDep = isectWvlDep && (flags & kBxT);
-        const float cosv = absdot(wi, si.sn);
-        if (isWvlDependent || curWvlDep) {
-            for (int i = 0; i < 4; ++i) prev[i] = pathWvlPdf[i];
-            const float keep = f[wvlIdx[0]];
-            for (int i = 0; i < kNS; ++i) f[i] = 0.f;
-            f[wvlIdx[0]] = keep;  // zeroAllBinsBut(wvlIdx[0])
-            pathWvlPdf[0] *= bsdfPdf;
-            for (int i = 1; i < 4; ++i) {
-                HeroBsdf* b = &hb[curWvlDep ? i : 0];
-                f[wvlIdx[i]] += hb_f1(h, b, wo, wi, wvlIdx[i]);
-                pathWvlPdf[i] *= bsdf_pdf<kFtAll>(b->b, wo, wi, kBxAll);
-            }
-            for (int i = 0; i < kNS; ++i) beta[i] *= f[i] * cosv;
-        } else {
-            for (int i = 0; i < kNS; ++i) beta[i] *= (f[i] * cosv) / bsdfPdf;
-        }
-        if (s60_black(beta)) break;
-        ray = Ray{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
-        if ((flags & kBxSpecular) && (flags & kBxT)) {
-            const float eta = hb[0].b.eta;
-            etaScale *= (dot(wo, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
-        }
-        float mc = beta[0] * etaScale;
-        for (int i = 1; i < kNS; ++i) mc = smax(mc, beta[i] * etaScale);
-        if (mc < sc.rr_threshold && bounces > 3) {
-            const float q = smax(0.05f, 1 - mc);
-            if (dm.get1() < q) break;
-            for (int i = 0; i < kNS; ++i) beta[i] /= 1 - q;
-        }
-        isWvlDependent |= curWvlDep;
-        isLastSpecular = (flags & kBxSpecular) != 0;
-    }
+    return t;
 }
 
-// One thread per (pixel, sample) slot of the batch: camera sample, the four
-// hero wavelengths (hero.cpp:113-150) and the path; writes pfilm and out60.
-__global__ __launch_bounds__(kTraceBlock) void k_hero(DevScene sc, DevHero h, DevPaths ps,
-                                                      const int2* __restrict__ pix, int npix, int s0, int nsamp,
-                                                      HaltonPixelConsts hp, int* spill, DevStats* stats) {
-    __shared__ int stk[kStackLds][kTraceBlock];
-    const uint32_t total = (uint32_t)npix * (uint32_t)nsamp;
-    const size_t gtid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int* myspill = spill + gtid * (64 - kStackLds);
-    HeroCounters ctr{0, 0, 0, 0};
-    bool overflow = false;
-    float L[kNS];
-    for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-        const uint32_t slot = base + threadIdx.x;
-        if (slot >= total) continue;
-        const uint32_t p = slot / (uint32_t)nsamp, sl = slot - p * (uint32_t)nsamp;
-        const int2 px = pix[p];
-        const uint32_t off = halton_pixel_offset(sc, px.x, px.y, hp.exp1, hp.scale0, hp.mi0, hp.mi1);
-        const uint32_t idx = off + (uint32_t)(s0 + (int)sl) * sc.hal_stride;
-        const float fx = (float)px.x + halton_dim(sc, idx, 0);
-        const float fy = (float)px.y + halton_dim(sc, idx, 1);
-        float lx = 0.5f, ly = 0.5f;
-        if (sc.lens_radius > 0) { lx = halton_dim(sc, idx, 3); ly = halton_dim(sc, idx, 4); }
-        const float uw = halton_dim(sc, idx, sc.wvl_dim);
-        const Ray r = camera_ray(sc, fx, fy, lx, ly);
-        float wvls[4];
+// Camera-sample set-up after k_camera: the four hero wavelengths
+// (hero.cpp:113-150) and the path state (hero_path.cpp:60-75).
+__global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPaths ps, DevHeroPaths hp,
+                                                   uint32_t total) {
+    const uint32_t N = (uint32_t)ps.n;
+    for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
+        const float uw = halton_dim(sc, ps.hidx[slot], sc.wvl_dim);
         for (int i = 0; i < 4; ++i) {
             // rotateValue: fmod(sample + i / 4, 1.0) in double (hero.cpp:45-47)
             const float s = (float)fmod((double)(uw + (float)i / (float)4), 1.0);
@@ -389,18 +253,418 @@ __global__ __launch_bounds__(kTraceBlock) void k_hero(DevScene sc, DevHero h, De
             bin = bin < 0 ? 0 : (bin > kNS - 1 ? kNS - 1 : bin);
             const float minv = h.wcdf[bin], maxv = h.wcdf[bin + 1], diff = maxv - minv;
             const float alpha = (s - minv) / diff;
-            wvls[i] = (float)400 + (float)300 * ((alpha + (float)bin) / (float)kNS);
+            hp.hs[(kHsWvl + i) * N + slot] = (float)400 + (float)300 * ((alpha + (float)bin) / (float)kNS);
+            hp.hs[(kHsPath + i) * N + slot] = 1.f;
+            hp.hs[(kHsPrev + i) * N + slot] = 1.f;
         }
-        Dims dm{&sc, idx, sc.wvl_dim + 1, false};
-        hero_li(sc, h, r, wvls, dm, stk, myspill, ctr, L);
-        overflow |= dm.overflow;
-        ps.pfilm[slot] = make_float2(fx, fy);
-        float* o = h.out60 + (size_t)slot * kNS;
-        for (int i = 0; i < kNS; ++i) o[i] = L[i];
+        hp.hs[kHsEtaScale * N + slot] = 1.f;
+        hp.hs[kHsBsdfPdf * N + slot] = 0.f;
+        hp.hs[kHsFlags * N + slot] = __uint_as_float(0u);
+        for (int b = 0; b < kNS; ++b) {
+            hp.beta[b * N + slot] = 1.f;
+            hp.L[b * N + slot] = 0.f;
+        }
     }
-    flush_stats(stats, ctr.closest, ctr.shadow, ctr.nodes, ctr.prims);
+}
+
+// One vertex of a hero path (hero_path.cpp:76-189, hero_path_mis.cpp:110-327):
+// first the pending light sample of the previous vertex (added if its shadow
+// ray came back unoccluded), then the hit of the continuation ray.  Emits the
+// shadow ray of SampleEmitterHero and the next continuation ray.
+__device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, const DevPaths& ps, const DevHeroPaths& hp,
+                          uint32_t slot, uint32_t* rays, uint32_t* nrays, bool* overflow) {
+    const uint32_t N = (uint32_t)ps.n;
+    uint32_t st = ps.st[slot];
+    float* Lg = hp.L + slot;
+    float* Bg = hp.beta + slot;
+    float* Ng = hp.nee + slot;
+    float* H = hp.hs + slot;
+    uint32_t hf = __float_as_uint(H[kHsFlags * N]);
+    *nrays = 0;
+    if (st & kStNee) {
+        if ((hf & kHfPend) && ps.hitA[slot] == 0)
+            for (int i0 = 0; i0 < kNS; i0 += kG) {
+                float l[kG], x[kG];
+                gload(Lg, N, i0, l);
+                gload(Ng, N, i0, x);
+#pragma unroll
+                for (int j = 0; j < kG; ++j) l[j] += x[j];
+                gstore(Lg, N, i0, l);
+            }
+        st &= ~kStNee;
+        hf &= ~kHfPend;
+    }
+    // the finished sample's radiance, slot-major for the film gather
+    auto finish = [&]() {
+        float* o = h.out60 + (size_t)slot * kNS;
+        for (int i0 = 0; i0 < kNS; i0 += kG) {
+            float l[kG];
+            gload(Lg, N, i0, l);
+#pragma unroll
+            for (int j = 0; j < kG; ++j) o[i0 + j] = l[j];
+        }
+    };
+    if (!(st & kStCont)) {
+        H[kHsFlags * N] = __uint_as_float(hf);
+        ps.st[slot] = st;
+        finish();
+        return;
+    }
+    st &= ~kStCont;
+    Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+    int bounces = (int)((st >> kStBounceShift) & 0xffu);
+    float wvls[4], pathWvlPdf[4], prev[4];
+    int wvlIdx[4];
+    for (int k = 0; k < 4; ++k) {
+        wvls[k] = H[(kHsWvl + k) * N];
+        wvlIdx[k] = wvl_index(wvls[k]);
+        pathWvlPdf[k] = H[(kHsPath + k) * N];
+        prev[k] = H[(kHsPrev + k) * N];
+    }
+    float etaScale = H[kHsEtaScale * N], bsdfPdf = H[kHsBsdfPdf * N];
+    bool isWvlDependent = (hf & kHfWvlDep) != 0;
+    const bool isLastSpecular = (hf & kHfLastSpec) != 0;
+    Ray ray = load_ray6(ps.ray, N, slot, kInf);
+    const V3 rayO = ray.o;
+    const int hpr = ps.hit[slot];
+    SurfHit si;
+    const bool found = hpr >= 0 && surface_at<true>(sc, hpr, ray, &si);
+    float tmp[kNS];  // infinite lights' FromRGB(Illuminant) radiance
+    // Lo += beta * Le, weighted (hero_path.cpp:84-104, hero_path_mis.cpp:120-166)
+    auto add_emitted = [&](auto Le, float emPdf) {
+        const float sw = pathWvlPdf[0] + pathWvlPdf[1] + pathWvlPdf[2] + pathWvlPdf[3];
+        const float s = (pathWvlPdf[0] + prev[0] * emPdf) + (pathWvlPdf[1] + prev[1] * emPdf) +
+                        (pathWvlPdf[2] + prev[2] * emPdf) + (pathWvlPdf[3] + prev[3] * emPdf);
+        const float mwc = bsdfPdf / (bsdfPdf + emPdf);
+        for (int i0 = 0; i0 < kNS; i0 += kG) {
+            float l[kG], bv[kG];
+            gload(Lg, N, i0, l);
+            gload(Bg, N, i0, bv);
+#pragma unroll
+            for (int j = 0; j < kG; ++j) {
+                const int i = i0 + j;
+                if (!h.mis)
+                    l[j] += isWvlDependent ? (bv[j] * Le(i)) / (wvl_pdf(h, wvlIdx, i) * sw) : bv[j] * Le(i);
+                else if (bounces == 0)
+                    l[j] += bv[j] * Le(i);
+                else
+                    l[j] += (bv[j] * Le(i)) * (isWvlDependent ? 1.0f / (wvl_pdf(h, wvlIdx, i) * s) : mwc);
+            }
+            gstore(Lg, N, i0, l);
+        }
+    };
+    bool cont = false;
+    if (!found) {
+        for (int li = 0; li < sc.n_lights; ++li) {
+            const DevLight& l = sc.lights[li];
+            if (l.kind != PT_LIGHT_INFINITE) continue;
+            s60_from_rgb_illum(h, inf_Le(l, ray.d), tmp);  // Spectrum(Lmap->Lookup, Illuminant)
+            if (s60_black(tmp)) continue;
+            const float emPdf = (h.mis && bounces > 0 && !isLastSpecular) ? inf_pdf_li(l, ray.d) : 0.f;
+            add_emitted([&](int i) { return tmp[i]; }, emPdf);
+        }
+    } else {
+        int mat, light;
+        prim_info<true>(sc, hpr, &mat, &light);
+        if (light >= 0) {
+            const DevLight& l = sc.lights[PT_IDX(light, sc.n_lights)];
+            const bool vis = l.two_sided || dot(si.n, -ray.d) > 0;  // DiffuseAreaLight::L
+            const float* Lrow = h.light_s60 + (size_t)light * kNS;
+            bool black = true;
+            for (int i = 0; i < kNS; ++i) black &= (vis ? Lrow[i] : 0.f) == 0.f;
+            if (!black) {
+                float emPdf = 0;
+                if (h.mis && bounces > 0 && !isLastSpecular) {  // PdfEmitterHero (hero_path_mis.cpp:46-76)
+                    const float tHit = hit_t(sc, hpr, ray);
+                    emPdf = (tHit * tHit) / (absdot(si.n, si.wo) * l.area);  // it.shape->Area()
+                    const float* d = hero_dist(h, rayO);
+                    const int nl = sc.n_lights;
+                    emPdf = emPdf * (d[light] / (d[2 * nl + 1] * nl));
+                }
+                add_emitted([&](int i) { return vis ? Lrow[i] : 0.f; }, emPdf);
+            }
+        }
+        const pt_material& M = sc.mats[PT_IDX(mat, sc.n_mats)];
+        if (bounces >= sc.max_depth) {
+        } else if (M.kind == PT_MAT_NONE) {  // bounces-- ; continue
+            store_ray6(ps.ray, N, slot, Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf});
+            rays[(*nrays)++] = slot << 2 | kRayCont;
+            cont = true;
+        } else {
+            const bool disp = M.kind == PT_MAT_DISPERSIVE_GLASS;
+            float etas[4] = {M.ior, M.ior, M.ior, M.ior};
+            if (disp) {  // one BSDF per wavelength (dispersive_glass.cpp:62-118)
+                const float lminsq = (float)(400 * 400), lmaxsq = (float)(700 * 700);
+                const float cauchyB = (lminsq * M.ior_max - lmaxsq * M.ior_min) / (lminsq - lmaxsq);
+                const float cauchyC = lminsq * (M.ior_max - cauchyB);
+                for (int i = 0; i < 4; ++i) etas[i] = cauchyB + cauchyC / (wvls[i] * wvls[i]);
+            }
+            HeroBsdf hb0;
+            hb_make(sc, h, mat, si, etas[0], &hb0);
+            const bool isectWvlDep = disp && hb0.b.n > 0;
+            // f and pdf of the i-th wavelength's BSDF at one bin
+            auto f1_pdf = [&](bool perWvl, int i, V3 wo, V3 wi, int bin, float* pdf) {
+                if (!perWvl || i == 0) {
+                    const float f = hb_f1(h, &hb0, wo, wi, bin);
+                    *pdf = bsdf_pdf<kFtAll>(hb0.b, wo, wi, kBxAll);
+                    return f;
+                }
+                HeroBsdf hbi;
+                hb_make(sc, h, mat, si, etas[i], &hbi);
+                const float f = hb_f1(h, &hbi, wo, wi, bin);
+                *pdf = bsdf_pdf<kFtAll>(hbi.b, wo, wi, kBxAll);
+                return f;
+            };
+            if (h.mis && bsdf_num<kFtAll>(hb0.b, kBxNonSpecular) > 0 && sc.n_lights > 0) {
+                // SampleEmitterHero (hero_path_mis.cpp:78-108); the shadow ray is
+                // traced by the next k_trace and the term added by the next step
+                const float* d = hero_dist(h, si.p);
+                const int nl = sc.n_lights;
+                float lpdf;
+                const int li = dist_sample(d, nl, dm.get1(), &lpdf);
+                float emPdf = lpdf;
+                if (lpdf != 0.f) {
+                    const float u0 = dm.get1(), u1 = dm.get1();
+                    float epdf = 0;
+                    V3 wi = v3(0, 0, 0), sp, sn, spe;
+                    const DevLight& l = sc.lights[PT_IDX(li, sc.n_lights)];
+                    const S3 Lrgb = area_sample_li<kFtAll>(sc, l, si, u0, u1, &wi, &epdf, &sp, &sn, &spe);
+                    if (epdf != 0.f) {
+                        const V3 origin = offset_ray_origin(si.p, si.perr, si.n, sp - si.p);
+                        const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
+                        const V3 dd = target - origin;
+                        float* a = ps.rayA;
+                        a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
+                        a[3 * N + slot] = dd.x; a[4 * N + slot] = dd.y; a[5 * N + slot] = dd.z;
+                        a[6 * N + slot] = 1 - kShadowEps;
+                        rays[(*nrays)++] = slot << 2 | kRayShadow;
+                        st |= kStNee;
+                        // the term as if unoccluded
+                        emPdf = emPdf * epdf;
+                        const bool inf = l.kind == PT_LIGHT_INFINITE;
+                        const bool vis = inf || l.two_sided || dot(sn, -wi) > 0;
+                        if (inf) s60_from_rgb_illum(h, Lrgb, tmp);
+                        const float* Lrow = h.light_s60 + (size_t)li * kNS;
+                        auto Li = [&](int i) { return (inf ? tmp[i] : (vis ? Lrow[i] : 0.f)) / emPdf; };
+                        bool haveLi = false;
+                        for (int i = 0; i < kNS; ++i) haveLi |= Li(i) != 0.f;
+                        if (haveLi && emPdf > 0.f) {
+                            const V3 wo = si.wo;
+                            const float cosv = absdot(wi, si.sn);
+                            const bool depN = isWvlDependent || isectWvlDep;
+                            const float mwn = depN ? 0.f : emPdf / (emPdf + bsdf_pdf<kFtAll>(hb0.b, wo, wi, kBxAll));
+                            bool fnb = false;  // !IsBlack(f); the term itself when no bin is wavelength-dependent
+                            hb_f_all(h, &hb0, wo, wi, [&](int i0, const float* f) {
+#pragma unroll
+                                for (int j = 0; j < kG; ++j) fnb |= f[j] != 0.f;
+                                if (!depN) {
+                                    float bv[kG], nv[kG];
+                                    gload(Bg, N, i0, bv);
+#pragma unroll
+                                    for (int j = 0; j < kG; ++j) nv[j] = ((bv[j] * Li(i0 + j)) * (f[j] * cosv)) * mwn;
+                                    gstore(Ng, N, i0, nv);
+                                }
+                            });
+                            if (fnb) {
+                                if (depN) {
+                                    float fv[4], bp[4];
+                                    for (int i = 0; i < 4; ++i) fv[i] = f1_pdf(isectWvlDep, i, wo, wi, wvlIdx[i], &bp[i]);
+                                    const float s = (pathWvlPdf[0] * emPdf + pathWvlPdf[0] * bp[0]) +
+                                                    (pathWvlPdf[1] * emPdf + pathWvlPdf[1] * bp[1]) +
+                                                    (pathWvlPdf[2] * emPdf + pathWvlPdf[2] * bp[2]) +
+                                                    (pathWvlPdf[3] * emPdf + pathWvlPdf[3] * bp[3]);
+                                    for (int i0 = 0; i0 < kNS; i0 += kG) {
+                                        float bv[kG], nv[kG];
+                                        gload(Bg, N, i0, bv);
+#pragma unroll
+                                        for (int j = 0; j < kG; ++j) {
+                                            const int b = i0 + j;
+                                            float f = 0.0f;  // f[wvlIdx[i]] += f_i, in order
+                                            for (int i = 0; i < 4; ++i)
+                                                if (wvlIdx[i] == b) f += fv[i];
+                                            const float mw = emPdf / (wvl_pdf(h, wvlIdx, b) * s);
+                                            nv[j] = ((bv[j] * Li(b)) * (f * cosv)) * mw;
+                                        }
+                                        gstore(Ng, N, i0, nv);
+                                    }
+                                }
+                                hf |= kHfPend;
+                            }
+                        }
+                    }
+                }
+            }
+            // BSDF sampling (hero_path.cpp:128-189, hero_path_mis.cpp:250-327)
+            const V3 wo = -ray.d;
+            V3 wi = v3(0, 0, 0);
+            int flags = 0;
+            const float u0 = dm.get1(), u1 = dm.get1();
+            bsdfPdf = 0;
+            bool fnb = false, curWvlDep = false, dep = false;
+            float keep0 = 0.f;  // f[wvlIdx[0]]
+            // the direction, pdf and lobe type do not depend on the reflectances:
+            // sample at chunk 0, then only the values of the other chunks (a
+            // specular lobe is cheap to re-run; a non-specular one is BSDF::f's
+            // lobe sum at the sampled local direction, as in BSDF::Sample_f)
+            V3 woL = v3(0, 0, 0), wiL = v3(0, 0, 0);
+            bool reflectS = false, specS = false;
+            {
+                hb_chunk(h, &hb0, 0);
+                const S3 v0 = bsdf_sample<kFtAll>(hb0.b, wo, &wi, u0, u1, &bsdfPdf, kBxAll, &flags, &wiL);
+                curWvlDep = isectWvlDep && (flags & kBxT);
+                dep = isWvlDependent || curWvlDep;
+                specS = (flags & kBxSpecular) != 0;
+                woL = w2l(hb0.b, wo);
+                reflectS = dot(wi, hb0.b.ng) * dot(wo, hb0.b.ng) > 0;
+                const float cosv = absdot(wi, si.sn);
+                for (int i0 = 0; bsdfPdf != 0.f && i0 < kNS; i0 += kG) {  // pdf 0: every chunk returns 0
+                    float f[kG];
+#pragma unroll
+                    for (int c = 0; c < kG / 3; ++c) {
+                        const int k = i0 / 3 + c;
+                        S3 v = v0;
+                        if (k > 0) {
+                            hb_chunk(h, &hb0, k);
+                            if (specS) {
+                                int fl2 = 0;
+                                float pdf2 = 0;
+                                V3 wi2;
+                                v = bsdf_sample<kFtAll>(hb0.b, wo, &wi2, u0, u1, &pdf2, kBxAll, &fl2);
+                            } else {
+                                v = hb_lobes_f(hb0.b, woL, wiL, reflectS);
+                            }
+                        }
+                        f[3 * c] = v.c[0]; f[3 * c + 1] = v.c[1]; f[3 * c + 2] = v.c[2];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kG; ++j) {
+                        fnb |= f[j] != 0.f;
+                        if (i0 + j == wvlIdx[0]) keep0 = f[j];
+                    }
+                    if (!dep) {  // beta *= f |cos| / pdf (unused if f is black)
+                        float bv[kG];
+                        gload(Bg, N, i0, bv);
+#pragma unroll
+                        for (int j = 0; j < kG; ++j) bv[j] *= (f[j] * cosv) / bsdfPdf;
+                        gstore(Bg, N, i0, bv);
+                    }
+                }
+            }
+            if (fnb && bsdfPdf != 0.f) {
+                const float cosv = absdot(wi, si.sn);
+                if (dep) {
+                    for (int i = 0; i < 4; ++i) prev[i] = pathWvlPdf[i];
+                    float fv[4];
+                    fv[0] = keep0;  // zeroAllBinsBut(wvlIdx[0])
+                    pathWvlPdf[0] *= bsdfPdf;
+                    for (int i = 1; i < 4; ++i) {
+                        float p;
+                        fv[i] = f1_pdf(curWvlDep, i, wo, wi, wvlIdx[i], &p);
+                        pathWvlPdf[i] *= p;
+                    }
+                    for (int i0 = 0; i0 < kNS; i0 += kG) {
+                        float bv[kG];
+                        gload(Bg, N, i0, bv);
+#pragma unroll
+                        for (int j = 0; j < kG; ++j) {
+                            const int b = i0 + j;
+                            float f = b == wvlIdx[0] ? fv[0] : 0.f;
+                            for (int i = 1; i < 4; ++i)
+                                if (wvlIdx[i] == b) f += fv[i];
+                            bv[j] *= f * cosv;
+                        }
+                        gstore(Bg, N, i0, bv);
+                    }
+                }
+                bool bnb = false;
+                for (int i = 0; i < kNS; ++i) bnb |= Bg[i * N] != 0.f;
+                if (bnb) {
+                    ray = Ray{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
+                    if ((flags & kBxSpecular) && (flags & kBxT)) {
+                        const float eta = hb0.b.eta;
+                        etaScale *= (dot(wo, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                    }
+                    float mc = Bg[0] * etaScale;
+                    for (int i = 1; i < kNS; ++i) mc = smax(mc, Bg[i * N] * etaScale);
+                    bool alive = true;
+                    if (mc < sc.rr_threshold && bounces > 3) {
+                        const float q = smax(0.05f, 1 - mc);
+                        if (dm.get1() < q) alive = false;
+                        else
+                            for (int i0 = 0; i0 < kNS; i0 += kG) {
+                                float bv[kG];
+                                gload(Bg, N, i0, bv);
+#pragma unroll
+                                for (int j = 0; j < kG; ++j) bv[j] /= 1 - q;
+                                gstore(Bg, N, i0, bv);
+                            }
+                    }
+                    if (alive) {
+                        isWvlDependent |= curWvlDep;
+                        hf = (hf & ~(kHfWvlDep | kHfLastSpec)) | (isWvlDependent ? kHfWvlDep : 0u) |
+                             ((flags & kBxSpecular) ? kHfLastSpec : 0u);
+                        store_ray6(ps.ray, N, slot, ray);
+                        rays[(*nrays)++] = slot << 2 | kRayCont;
+                        cont = true;
+                        ++bounces;
+                        for (int k = 0; k < 4; ++k) {
+                            H[(kHsPath + k) * N] = pathWvlPdf[k];
+                            H[(kHsPrev + k) * N] = prev[k];
+                        }
+                        H[kHsEtaScale * N] = etaScale;
+                        H[kHsBsdfPdf * N] = bsdfPdf;
+                    }
+                }
+            }
+        }
+    }
+    if (cont) st |= kStCont;
+    if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
+    st = (st & ~(kStDimMask | (0xffu << kStBounceShift))) | ((uint32_t)dm.dim & kStDimMask) |
+         ((uint32_t)bounces << kStBounceShift);
+    H[kHsFlags * N] = __uint_as_float(hf);
+    ps.st[slot] = st;
+    if (!(st & (kStCont | kStNee))) finish();
+}
+
+__device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHero& h, const DevPaths& ps,
+                                                 const DevHeroPaths& hp, const uint32_t* __restrict__ pq,
+                                                 const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                                 uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
+                                                 DevStats* stats) {
+    const uint32_t n = *pq_count;
+    bool overflow = false;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t rays[2];
+        uint32_t nrays = 0;
+        bool keep = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = pq[i];
+            hero_step(sc, h, ps, hp, slot, rays, &nrays, &overflow);
+            keep = (ps.st[slot] & (kStCont | kStNee)) != 0;
+        }
+        const uint32_t pos = wave_reserve(rq_out_count, nrays);
+        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
+        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
+        if (keep) pq_out[ppos] = slot;
+    }
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
+
+// register-budget variants (PT_HERO_WAVES): compiler default, 2 or 4 waves per SIMD
+#define PT_HERO_SHADE(name, attr)                                                                                   \
+    __global__ __launch_bounds__(kShadeBlock) attr void name(                                                      \
+        DevScene sc, DevHero h, DevPaths ps, DevHeroPaths hp, const uint32_t* __restrict__ pq,                     \
+        const uint32_t* __restrict__ pq_count, uint32_t* rq_out, uint32_t* rq_out_count, uint32_t* pq_out,        \
+        uint32_t* pq_out_count, DevStats* stats) {                                                                  \
+        shade_hero_batch(sc, h, ps, hp, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);           \
+    }
+PT_HERO_SHADE(k_shade_hero, )
+PT_HERO_SHADE(k_shade_hero_w2, __attribute__((amdgpu_waves_per_eu(2))))
+PT_HERO_SHADE(k_shade_hero_w4, __attribute__((amdgpu_waves_per_eu(4))))
+#undef PT_HERO_SHADE
 
 // Film for SampledSpectrum samples: k_film's ordered per-pixel gather with a
 // 60-bin FilmTile contribSum (lane = bin), converted by ToXYZ at the merge

@@ -265,6 +265,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
     uint32_t slot = 0, kind = 0;
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
     V3 inv = v3(0, 0, 0);
+    TriShear sh{0, 0, 0, 0};
     bool n0 = false, n1 = false, n2 = false;
     int cur = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
     for (;;) {
@@ -287,6 +288,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                                   v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
                                   kind == kRayShadow ? a[6 * N + slot] : kInf};
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                        sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
                         cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
                         active = sc.n_nodes > 0;  // empty scene: every ray misses
@@ -328,9 +330,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                 ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
             } else {
                 const float4 r2 = bprims[3 * pi + 2];
-                float b0, b1, b2;
-                ok = tri_test(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t, &b0, &b1,
-                              &b2);
+                ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
                 if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
             }
             if (ok) {
@@ -416,6 +416,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
     uint32_t slot = 0, kind = 0;
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
     V3 inv = v3(0, 0, 0);
+    TriShear sh{0, 0, 0, 0};
     bool n0 = false, n1 = false, n2 = false;
     int cur = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
     for (;;) {
@@ -438,6 +439,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
                                   v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
                                   kind == kRayShadow ? a[6 * N + slot] : kInf};
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                        sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
                         cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
                         active = sc.n_nodes > 0;  // empty scene: every ray misses
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
                 if (fl & kPrimAnalytic) {
                     ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
                 } else {
-                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, &t);
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
                     ok &= (kind == kRayShadow) | !(fl & kPrimDegenerate);
                 }
                 hitPrim = ok ? pi : hitPrim;
@@ -1283,6 +1285,19 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))
 }
 template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_w4(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+
+template <int kFt>
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_shade_w5(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+template <int kFt>
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_w6(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
     shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);

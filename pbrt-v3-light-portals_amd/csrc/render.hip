@@ -200,7 +200,7 @@ struct pt_scene {
     // hero integrators (SampledSpectrum scenes): tables, light distributions, per-slot radiance
     bool hero = false;
     pt::DevHero hh{};
-    pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist, h_out60;
+    pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist, h_out60, h_L60, h_beta60, h_nee60, h_hs;
     pt::HaltonPixelConsts hpc{};
     pt::FilmConsts film{};
     pt::Frame fr{};
@@ -214,6 +214,7 @@ struct pt_scene {
     size_t target_slots = (size_t)8 << 20;
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
+    int hero_waves = 4;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4)
     int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
@@ -251,7 +252,13 @@ using ShadeKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t
                              uint32_t*, DevStats*);
 template <int kFt>
 static ShadeKernel shade_kernel_ft(int variant) {
-    return variant == 4 ? k_shade_w4<kFt> : (variant == 3 ? k_shade_w3<kFt> : k_shade<kFt>);
+    switch (variant) {
+        case 3: return k_shade_w3<kFt>;
+        case 4: return k_shade_w4<kFt>;
+        case 5: return k_shade_w5<kFt>;
+        case 6: return k_shade_w6<kFt>;
+        default: return k_shade<kFt>;
+    }
 }
 // Instantiated feature sets: all-matte, + infinite light, + spheres, + both,
 // everything.  Other combinations take the full kernel.
@@ -977,9 +984,15 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
              direct ? s->dev.dl_frames : 0);
     HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
     DevPaths ps = w.paths((int)max_slots);
-    if (s->hero) {
+    DevHeroPaths hps{};
+    if (s->hero) {  // 60-bin radiance / throughput / pending light term + scalars per slot
         s->h_out60.alloc(max_slots * (size_t)kNSpec);
+        s->h_L60.alloc(max_slots * (size_t)kNSpec);
+        s->h_beta60.alloc(max_slots * (size_t)kNSpec);
+        s->h_nee60.alloc(max_slots * (size_t)kNSpec);
+        s->h_hs.alloc(max_slots * (size_t)kHs);
         s->hh.out60 = s->h_out60.p;
+        hps = DevHeroPaths{s->h_beta60.p, s->h_L60.p, s->h_nee60.p, s->h_hs.p};
     }
     hipEvent_t ev0, ev1;
     HIPCHK(hipEventCreate(&ev0));
@@ -1013,30 +1026,11 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         for (int s0 = s_begin; s0 < s_end; s0 += g.S) {
             const int ns = std::min(g.S, s_end - s0);
             const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
-            if (s->hero) {
-                // hero integrators: one megakernel pass per batch, then the 60-bin film
-                auto e = tev_get(tcount++);
-                HIPCHK(hipEventRecord(e.first, stream));
-                hipLaunchKernelGGL(k_hero, dim3(std::max(1, std::min(ceil_div(nb, kTraceBlock), maxBlocksTrace))),
-                                   dim3(kTraceBlock), 0, stream, s->dev, s->hh, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc,
-                                   w.spill.p, w.stats.p);
-                HIPCHK(hipEventRecord(e.second, stream));
-                rr.launches++;
-                HIPCHK(hipGetLastError());
-                sync_check("k_hero", 0);
-                const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
-                if (bw > 0 && bh > 0) {
-                    hipLaunchKernelGGL(k_film_s60, dim3(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32))),
-                                       dim3(256), 0, stream, s->hh, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0,
-                                       bw, bh, d_accum);
-                    HIPCHK(hipGetLastError());
-                    sync_check("k_film_s60", 0);
-                }
-                rr.samples += nb;
-                continue;
-            }
             hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
                                stream, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
+            if (s->hero)  // the hero wavelengths and 60-bin path state of every camera sample
+                hipLaunchKernelGGL(k_hero_init, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))),
+                                   dim3(256), 0, stream, s->dev, s->hh, ps, hps, nb);
             hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
             HIPCHK(hipGetLastError());
             sync_check("k_camera", 0);
@@ -1075,9 +1069,15 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     sync_check("k_trace", iter);
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
-                const ShadeKernel kshade = direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
-                hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1, rq_out,
-                                   counts + 2, pq_out, counts + 3, w.stats.p);
+                if (s->hero) {
+                    hipLaunchKernelGGL(s->hero_waves == 1 ? k_shade_hero : (s->hero_waves == 2 ? k_shade_hero_w2 : k_shade_hero_w4), sg, dim3(kShadeBlock), 0, stream, s->dev, s->hh, ps, hps, pq_in,
+                                       counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
+                } else {
+                    const ShadeKernel kshade =
+                        direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
+                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1,
+                                       rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
+                }
                 HIPCHK(hipGetLastError());
                 sync_check("k_shade", iter);
                 HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1091,9 +1091,13 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             }
             const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
             if (bw > 0 && bh > 0) {
-                hipLaunchKernelGGL(k_film, dim3(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32))),
-                                   dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
-                                   d_accum);
+                const dim3 fg(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32)));
+                if (s->hero)
+                    hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, stream, s->hh, ps, s->film, dslot.p, g.p0, g.np,
+                                       ns, g.bx0, g.by0, bw, bh, d_accum);
+                else
+                    hipLaunchKernelGGL(k_film, fg, dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0,
+                                       g.by0, bw, bh, d_accum);
                 HIPCHK(hipGetLastError());
                 sync_check("k_film", 0);
             }
@@ -1285,6 +1289,7 @@ pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         const char* e = std::getenv("PT_TRACE_LDS");
         s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                                  ? scene_bytes : 0;
+        if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
         const char* v = std::getenv("PT_SHADE_VARIANT");
         if (v) s->shade_variant = std::atoi(v);
         s->has_spheres = (s->features & kFtSphere) != 0;
