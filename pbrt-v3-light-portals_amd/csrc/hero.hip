@@ -37,6 +37,7 @@ struct DevHero {
     const float* XYZ;        // 3 x 60 CIE matching functions (SampledSpectrum::Init)
     const float* illum;      // 7 x 60 RGB->illuminant basis (W C M Y R G B)
     const float* mat_s60;    // n_materials x 3 x 60
+    const int* mat_nb;       // n_materials: bit j = spectrum j is not black (after Clamp)
     const float* light_s60;  // n_lights x 60
     const float* wcdf;       // SpectralDistribution CDF, 61 entries
     // light sample distribution: one (func, cdf, funcInt) per voxel (spatial)
@@ -96,18 +97,12 @@ struct HeroBsdf {
     pt_material rep;  // lobe-selection stand-in; chunk values are written into it
     int mi;
 };
-__device__ __forceinline__ bool nonblack_clamped(const float* v) {
-    for (int i = 0; i < kNS; ++i)
-        if ((v[i] < 0 ? 0.f : v[i]) != 0.f) return true;
-    return false;
-}
 __device__ __forceinline__ void hb_make(const DevScene& sc, const DevHero& h, int mi, const SurfHit& si, float eta,
                                         HeroBsdf* hb) {
     hb->rep = sc.mats[PT_IDX(mi, sc.n_mats)];
     hb->mi = mi;
-    const float* ms = h.mat_s60 + (size_t)mi * 3 * kNS;
-    const float one = nonblack_clamped(ms) ? 1.f : 0.f, r = nonblack_clamped(ms + kNS) ? 1.f : 0.f,
-                t = nonblack_clamped(ms + 2 * kNS) ? 1.f : 0.f;
+    const int nb = h.mat_nb[mi];
+    const float one = (nb & 1) ? 1.f : 0.f, r = (nb & 2) ? 1.f : 0.f, t = (nb & 4) ? 1.f : 0.f;
     for (int c = 0; c < 3; ++c) { hb->rep.kd[c] = one; hb->rep.kr[c] = r; hb->rep.kt[c] = t; }
     if (hb->rep.kind == PT_MAT_DISPERSIVE_GLASS) { hb->rep.kind = PT_MAT_GLASS; hb->rep.ior = eta; }
     make_bsdf<kFtAll>(&hb->rep, si, 550.f, &hb->b);
@@ -126,6 +121,33 @@ __device__ __forceinline__ void hb_f(const DevHero& h, HeroBsdf* hb, V3 wo, V3 w
         hb_chunk(h, hb, k);
         const S3 v = bsdf_f<kFtAll>(hb->b, wo, wi, kBxAll);
         f[3 * k] = v.c[0]; f[3 * k + 1] = v.c[1]; f[3 * k + 2] = v.c[2];
+    }
+}
+// 12 bins of the spectra the material kind reads (Kd: matte; Kr, Kt: glass;
+// Kr: mirror; all three otherwise), as 16-byte loads, and chunk c of them
+// written into the material copy.
+struct HbGroup {
+    float4 v[3][kG / 4];
+};
+__device__ __forceinline__ void hb_group(const DevHero& h, const HeroBsdf* hb, int i0, HbGroup* g) {
+    const int kind = hb->rep.kind;
+    const int use = kind == PT_MAT_MATTE ? 1 : (kind == PT_MAT_GLASS ? 6 : (kind == PT_MAT_MIRROR ? 2 : 7));
+    const float4* ms = (const float4*)(h.mat_s60 + (size_t)hb->mi * 3 * kNS + i0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int q = 0; q < kG / 4; ++q) g->v[j][q] = (use >> j & 1) ? ms[j * kNS / 4 + q] : make_float4(0, 0, 0, 0);
+}
+__device__ __forceinline__ float g_at(const HbGroup& g, int j, int b) {
+    const float4 v = g.v[j][b / 4];
+    const int r = b % 4;
+    return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ void hb_chunk_g(HeroBsdf* hb, const HbGroup& g, int c) {
+    for (int q = 0; q < 3; ++q) {
+        hb->rep.kd[q] = g_at(g, 0, 3 * c + q);
+        hb->rep.kr[q] = g_at(g, 1, 3 * c + q);
+        hb->rep.kt[q] = g_at(g, 2, 3 * c + q);
     }
 }
 __device__ __forceinline__ float hb_f1(const DevHero& h, HeroBsdf* hb, V3 wo, V3 wi, int bin) {
@@ -154,9 +176,11 @@ __device__ __forceinline__ void hb_f_all(const DevHero& h, HeroBsdf* hb, V3 woW,
     const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
     for (int i0 = 0; i0 < kNS; i0 += kG) {  // out(i0, f) receives bins i0 .. i0 + kG - 1
         float f[kG];
+        HbGroup g;
+        hb_group(h, hb, i0, &g);
 #pragma unroll
         for (int c = 0; c < kG / 3; ++c) {
-            hb_chunk(h, hb, i0 / 3 + c);
+            hb_chunk_g(hb, g, c);
             const S3 v = wo.z == 0 ? s3(0.f) : hb_lobes_f(b, wo, wi, reflect);
             f[3 * c] = v.c[0]; f[3 * c + 1] = v.c[1]; f[3 * c + 2] = v.c[2];
         }
@@ -519,12 +543,14 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                 const float cosv = absdot(wi, si.sn);
                 for (int i0 = 0; bsdfPdf != 0.f && i0 < kNS; i0 += kG) {  // pdf 0: every chunk returns 0
                     float f[kG];
+                    HbGroup g;
+                    hb_group(h, &hb0, i0, &g);
 #pragma unroll
                     for (int c = 0; c < kG / 3; ++c) {
                         const int k = i0 / 3 + c;
                         S3 v = v0;
                         if (k > 0) {
-                            hb_chunk(h, &hb0, k);
+                            hb_chunk_g(&hb0, g, c);
                             if (specS) {
                                 int fl2 = 0;
                                 float pdf2 = 0;

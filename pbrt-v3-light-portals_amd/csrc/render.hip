@@ -201,6 +201,7 @@ struct pt_scene {
     bool hero = false;
     pt::DevHero hh{};
     pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist, h_out60, h_L60, h_beta60, h_nee60, h_hs;
+    pt::DBuf<int> h_matnb;
     pt::HaltonPixelConsts hpc{};
     pt::FilmConsts film{};
     pt::Frame fr{};
@@ -390,6 +391,16 @@ static void build_hero(pt_scene* s, const pt_scene_desc* d, const std::vector<De
     s->h_xyz.upload(xyz);
     s->h_illum.upload(illum);
     s->h_mat.upload(d->material_s60, (size_t)d->n_materials * 3 * kNSpec);
+    {   // per material: bit j set when spectrum j is not black after Clamp() (the lobe set's IsBlack tests)
+        std::vector<int> nb((size_t)std::max(1, d->n_materials), 0);
+        for (int m = 0; m < d->n_materials; ++m)
+            for (int j = 0; j < 3; ++j)
+                for (int i = 0; i < kNSpec; ++i) {
+                    const float v = d->material_s60[((size_t)m * 3 + j) * kNSpec + i];
+                    if ((v < 0 ? 0.f : v) != 0.f) { nb[m] |= 1 << j; break; }
+                }
+        s->h_matnb.upload(nb);
+    }
     s->h_light.upload(d->light_s60, (size_t)std::max(1, d->n_lights) * kNSpec);
     const int nl = d->n_lights;
     std::vector<std::vector<float>> power((size_t)nl, std::vector<float>(kNSpec));
@@ -421,6 +432,7 @@ static void build_hero(pt_scene* s, const pt_scene_desc* d, const std::vector<De
     h.XYZ = s->h_xyz.p;
     h.illum = s->h_illum.p;
     h.mat_s60 = s->h_mat.p;
+    h.mat_nb = s->h_matnb.p;
     h.light_s60 = s->h_light.p;
     h.wcdf = s->h_wcdf.p;
     h.mis = d->integrator.kind == PT_INTEGRATOR_HERO_PATH_MIS;
