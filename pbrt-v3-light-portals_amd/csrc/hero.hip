@@ -4,17 +4,18 @@
 // The reference runs hero_path / hero_path_mis only in its SampledSpectrum
 // build: every radiance quantity is 60 bins over 400-700 nm and four hero
 // wavelengths per camera sample drive dispersion (integrators/hero.cpp,
-// hero_path.cpp, hero_path_mis.cpp).  Carrying 2 x 240 B of spectral path
-// state through the wavefront queues would double the HBM traffic of every
-// bounce for a mode with no shared work between paths, so this path is a
-// megakernel: one thread per camera sample, the bounce loop in registers /
-// private memory, traversal inline (the LDS-stack `traverse` of kernels.hip),
-// the 60-bin radiance of each sample written once to `out60` and filtered by
-// k_film_s60 in the reference's FilmTile order.  BSDF values are evaluated
-// with the RGB lobe code three bins at a time (every lobe is f = R * scalar),
-// the lobe set being chosen from the full 60-bin reflectances; a lobe's
-// scalar factors do not depend on the bin, so each chunk is bit-identical to
-// the 60-bin evaluation.
+// hero_path.cpp, hero_path_mis.cpp).  The paths run on the same wavefront as
+// PathIntegrator: k_camera + k_hero_init start them, k_trace traces their
+// continuation and shadow rays, k_shade_hero advances each by one vertex,
+// with the 60-bin throughput / radiance / pending light-sample term in
+// bin-major SoA (coalesced across the wave) and the light sample's term added
+// by the next step when its shadow ray comes back unoccluded -- the order in
+// which the reference adds it.  BSDF values are evaluated with the RGB lobe
+// code three bins at a time (every lobe is f = R * scalar), the lobe set being
+// chosen from the full 60-bin reflectances; the direction, pdf and lobe type
+// are sampled once per vertex.  A finished sample's radiance is copied
+// slot-major for k_film_s60, which filters it in the reference's FilmTile
+// order.
 
 namespace pt {
 
