@@ -1,11 +1,11 @@
 #!/bin/bash
-# GPU: all gpu tests, then the config-5 (10M-triangle atrium) bench at a
-# reduced spp, its kernel-trace stats and the FETCH_SIZE / WRITE_SIZE passes.
+# GPU: all gpu tests, then a bench (default: config 5, the 10M-triangle atrium, at a
+# reduced spp; BENCH_ARGS overrides), its kernel-trace stats and the FETCH_SIZE / WRITE_SIZE passes.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-ARGS="--config c5 --spp ${C5_SPP:-16}"
+ARGS="${BENCH_ARGS:---config c5 --spp ${C5_SPP:-16}}"
 ok() { case "$1" in 0) return 0;; *) echo "STOP rc=$1"; return 1;; esac; }
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
