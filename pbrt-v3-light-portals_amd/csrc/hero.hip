@@ -754,18 +754,30 @@ __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmCo
                             }
                             uint64_t m = __ballot(touch);
                             if (m) any = true;
+                            // touching samples in order, four per round: their loads are
+                            // issued together, the sums stay in sample order
                             while (m) {
-                                const int j = __ffsll((unsigned long long)m) - 1;
-                                m &= m - 1;
-                                const uint32_t sj = (uint32_t)__shfl((int)slot, j);
-                                const float kj = lane_val(k, j), wj = lane_val(w, j);
-                                if (lane < kNS) {
-                                    float v = h.out60[(size_t)sj * kNS + lane];
-                                    if (kj == 0.f) v = 0.f;        // L = Spectrum(0.f)
-                                    else if (kj != 1.f) v = v * kj;  // L *= maxSampleLuminance / L.y()
-                                    binsum += (v * 1.f) * wj;
+                                int js[4];
+                                float vs[4];
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) {
+                                    js[q] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                                    m &= m - 1;
+                                    const uint32_t sj = (uint32_t)__shfl((int)slot, js[q] < 0 ? 0 : js[q]);
+                                    vs[q] = (js[q] >= 0 && lane < kNS) ? h.out60[(size_t)sj * kNS + lane] : 0.f;
                                 }
-                                wsum += wj;
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) {
+                                    if (js[q] < 0) break;
+                                    const float kj = lane_val(k, js[q]), wj = lane_val(w, js[q]);
+                                    if (lane < kNS) {
+                                        float v = vs[q];
+                                        if (kj == 0.f) v = 0.f;        // L = Spectrum(0.f)
+                                        else if (kj != 1.f) v = v * kj;  // L *= maxSampleLuminance / L.y()
+                                        binsum += (v * 1.f) * wj;
+                                    }
+                                    wsum += wj;
+                                }
                             }
                         }
                     }

@@ -212,7 +212,7 @@ struct pt_scene {
     pt::Work work;
     int device = 0;
     int num_cus = 256;
-    size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (16 M for the 60-bin hero state)
+    size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (8 M for the 60-bin hero state)
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int hero_waves = 4;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4)
@@ -956,7 +956,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         int bx0, by0, bx1, by1;
     };
     std::vector<Group> groups;
-    const size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)16 << 20 : (size_t)64 << 20);
+    const size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)64 << 20);
     size_t max_slots = 0;
     for (size_t i = 0; i < tiles.size();) {
         size_t j = i;
