@@ -33,6 +33,8 @@ typedef struct oracle_stats {
     uint64_t node_visits;
     uint64_t prim_tests;
     uint64_t samples;
+    uint64_t closest_node_visits;  /* node_visits / prim_tests of the closest-hit rays only; */
+    uint64_t closest_prim_tests;   /* the any-hit share is the difference */
 } oracle_stats;
 
 /* Render the scene exactly as SamplerIntegrator::Render with a PathIntegrator
@@ -97,6 +99,14 @@ int oracle_ray_triangle(const float o[3], const float d[3], float tmax,
 /* Camera ray for a film position (GenerateRayDifferential + CameraToWorld). */
 int oracle_camera_ray(const pt_scene_desc* desc, float film_x, float film_y,
                       float o[3], float d[3]);
+
+/* The reference's unit tests for this path, restated (src/tests/shapes.cpp,
+ * src/tests/sampling.cpp); see tests/test_reference_unit_tests.py. */
+int oracle_test_reintersect(int i, int n_dirs, float* tri9, float* rays7, int* self_hits);
+int oracle_test_triangle_sampling(int i, int count, double* unif, double* tri_est, float* tri9, float* pc3,
+                                  int* bad_pdf);
+int oracle_triangle_intersect(const float tri9[9], const float ray7[7], int any, float* t);
+int oracle_dist1d(const float* func, int n, int mode, float u, float* out);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,8 @@ LIB_PATH = os.path.join(HERE, "libptoracle.so")
 class oracle_stats(ctypes.Structure):
     _fields_ = [("camera_rays", ctypes.c_uint64), ("closest_rays", ctypes.c_uint64),
                 ("shadow_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
-                ("prim_tests", ctypes.c_uint64), ("samples", ctypes.c_uint64)]
+                ("prim_tests", ctypes.c_uint64), ("samples", ctypes.c_uint64),
+                ("closest_node_visits", ctypes.c_uint64), ("closest_prim_tests", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -66,6 +67,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_ray_triangle.argtypes = [vp, vp, ctypes.c_float, vp, vp, vp, vp, vp]
         L.oracle_camera_ray.argtypes = [vp, ctypes.c_float, ctypes.c_float, vp, vp]
         L.oracle_trace.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
+        L.oracle_test_reintersect.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_test_triangle_sampling.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(ctypes.c_double), vp, vp,
+                                                    ctypes.POINTER(ctypes.c_int)]
+        L.oracle_triangle_intersect.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.oracle_dist1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_float, vp]
         _lib = L
     return _lib
 
@@ -178,3 +185,52 @@ def ray_triangle(o, d, tmax, p0, p1, p2):
     hit = lib().oracle_ray_triangle(arrs[0].ctypes.data, arrs[1].ctypes.data, float(tmax), arrs[2].ctypes.data,
                                     arrs[3].ctypes.data, arrs[4].ctypes.data, t.ctypes.data, b.ctypes.data)
     return bool(hit), float(t[0])
+
+
+# ---- the reference's unit tests for this path, restated in the oracle ----
+
+def reintersect_case(i: int, n_dirs: int):
+    """Triangle.Reintersect (src/tests/shapes.cpp:155-206) for RNG seed i:
+    (triangle (3,3), spawned rays (2*n_dirs, 7), self-hit count) or None
+    when the reference skips the seed."""
+    tri = np.zeros(9, np.float32)
+    rays = np.zeros((2 * n_dirs, 7), np.float32)
+    bad = ctypes.c_int()
+    ok = lib().oracle_test_reintersect(i, n_dirs, tri.ctypes.data, rays.ctypes.data, ctypes.byref(bad))
+    return (tri.reshape(3, 3), rays, bad.value) if ok else None
+
+
+def triangle_sampling_case(i: int, count: int = 512 * 1024):
+    """Triangle.Sampling (src/tests/shapes.cpp:211-270) for RNG seed i:
+    (uniform-sphere estimate, Triangle::Sample estimate, triangle, pc,
+    non-positive pdf count) or None when skipped."""
+    a, b = ctypes.c_double(), ctypes.c_double()
+    tri = np.zeros(9, np.float32)
+    pc = np.zeros(3, np.float32)
+    bad = ctypes.c_int()
+    ok = lib().oracle_test_triangle_sampling(i, count, ctypes.byref(a), ctypes.byref(b), tri.ctypes.data,
+                                             pc.ctypes.data, ctypes.byref(bad))
+    return (a.value, b.value, tri.reshape(3, 3), pc, bad.value) if ok else None
+
+
+def triangle_intersect(tri9, ray7, any_hit: bool = False):
+    """Triangle::Intersect (any_hit False) / IntersectP of one triangle: (hit, t)."""
+    tri9 = np.ascontiguousarray(tri9, np.float32).reshape(9)
+    ray7 = np.ascontiguousarray(ray7, np.float32).reshape(7)
+    t = ctypes.c_float()
+    hit = lib().oracle_triangle_intersect(tri9.ctypes.data, ray7.ctypes.data, int(any_hit), ctypes.byref(t))
+    return bool(hit), t.value
+
+
+def dist1d(func, mode: str, u: float):
+    """Distribution1D (sampling.h:55-110): mode 'discrete' -> (offset, pdf,
+    uRemapped); 'continuous' -> (x, pdf, offset); 'pdf' -> DiscretePDF(int(u))."""
+    f = np.ascontiguousarray(func, np.float32)
+    out = np.zeros(3, np.float32)
+    m = {"discrete": 0, "continuous": 1, "pdf": 2}[mode]
+    assert lib().oracle_dist1d(f.ctypes.data, len(f), m, float(u), out.ctypes.data) == 0
+    if mode == "discrete":
+        return int(out[0]), float(out[1]), float(out[2])
+    if mode == "continuous":
+        return float(out[0]), float(out[1]), int(out[2])
+    return float(out[0])

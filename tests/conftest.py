@@ -47,13 +47,18 @@ def scene_variant(tmp_path, name="portal_cornell.pbrt", res=None, spp=None, stra
     if maxdepth is not None:
         import re
         txt = re.sub(r'"integer maxdepth" \[\d+\]', '"integer maxdepth" [%d]' % maxdepth, txt)
+    import re
+    # the variant lives elsewhere: keep the scene's own relative PLY files and
+    # Includes resolving against its directory under scenes/ (files named by
+    # `extra` stay relative to the variant)
+    sdir = os.path.dirname(os.path.join(SCENES, name))
+    txt = re.sub(r'"string filename" \["(?!/)([^"]+\.ply)"\]',
+                 lambda m: '"string filename" ["%s/%s"]' % (sdir, m.group(1)), txt)
     if extra:
         for a, b in extra:
             txt = txt.replace(a, b)
-    import re
-    # the variant lives elsewhere: keep relative Includes resolving against scenes/
-    txt = re.sub(r'Include "(?!/)([^"]+)"', lambda m: 'Include "%s/%s"' % (SCENES, m.group(1)), txt)
-    p = os.path.join(str(tmp_path), "v_%s_%s_%s_%s_%s" % (res, spp, strategy, maxdepth, name))
+    txt = re.sub(r'Include "(?!/)([^"]+)"', lambda m: 'Include "%s/%s"' % (sdir, m.group(1)), txt)
+    p = os.path.join(str(tmp_path), "v_%s_%s_%s_%s_%s" % (res, spp, strategy, maxdepth, name.replace("/", "_")))
     p = p.replace(" ", "").replace("(", "").replace(")", "").replace(",", "x")
     with open(p, "w") as f:
         f.write(txt)

@@ -541,3 +541,32 @@ def test_killeroo_atrium_matches_oracle(tmp_path):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+LAMP_AS_PATH = [('Integrator "directlighting"', 'Integrator "path" "integer maxdepth" [5]'),
+                ('"integer maxdepth" [100]', '')]
+
+
+@pytest.mark.parametrize("integrator", ["directlighting", "path"])
+@pytest.mark.parametrize("strategy", ["projection", "light", "portal"])
+def test_lamp_matches_oracle(tmp_path, integrator, strategy):
+    """The reference's own portal scene (scenes/lamp/lamp.pbrt, imported
+    verbatim): two axis-2 portals, the second '+'-facing (AAPortal facingFw,
+    aaportal.cpp:8-13; AAPlaneShape::InFront / Normal, plane.cpp:74-115),
+    plymesh room / lampshade, metal leg and base.  As written
+    (DirectLighting maxdepth 100, strategy projection, 5 spp) and as path
+    maxdepth 5 with each strategy, at 100x100: device == oracle bit for bit,
+    identical ray / node / primitive counters."""
+    from conftest import scene_variant
+    hs, sc = _scene(scene_variant(tmp_path, name="lamp/lamp.pbrt", res=(100, 100),
+                                  spp=5 if integrator == "directlighting" else 8, strategy=strategy,
+                                  extra=LAMP_AS_PATH if integrator == "path" else None))
+    assert ptgpu.integrator_desc(hs).kind == (1 if integrator == "directlighting" else 0)
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
+    print(f"lamp/{integrator}/{strategy}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
+    assert ref.mean() > 0
+    assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
