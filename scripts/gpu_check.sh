@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
 ok() { case "$1" in 0) return 0;; *) echo "STOP rc=$1"; return 1;; esac; }
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --maxfail=10 -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log; ok $rc || exit $rc
