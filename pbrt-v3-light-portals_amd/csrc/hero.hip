@@ -17,6 +17,9 @@
 // slot-major for k_film_s60, which filters it in the reference's FilmTile
 // order.
 
+#pragma once
+#include "kernels.hip"
+
 namespace pt {
 
 constexpr int kNS = 60;
@@ -264,7 +267,9 @@ __device__ __forceinline__ float hit_t(const DevScene& sc, int prim, const Ray& 
 // Camera-sample set-up after k_camera: the four hero wavelengths
 // (hero.cpp:113-150) and the path state (hero_path.cpp:60-75).
 __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPaths ps, DevHeroPaths hp,
-                                                   uint32_t total) {
+                                                   uint32_t total)
+#ifdef PT_TU_HERO
+{
     const uint32_t N = (uint32_t)ps.n;
     for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
         const float uw = halton_dim(sc, ps.hidx[slot], sc.wvl_dim);
@@ -291,6 +296,9 @@ __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPa
         }
     }
 }
+#else
+;
+#endif
 
 // One vertex of a hero path (hero_path.cpp:76-189, hero_path_mis.cpp:110-327):
 // first the pending light sample of the previous vertex (added if its shadow
@@ -685,20 +693,26 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
     __global__ __launch_bounds__(kShadeBlock) attr void name(                                                      \
         DevScene sc, DevHero h, DevPaths ps, DevHeroPaths hp, const uint32_t* __restrict__ pq,                     \
         const uint32_t* __restrict__ pq_count, uint32_t* rq_out, uint32_t* rq_out_count, uint32_t* pq_out,        \
-        uint32_t* pq_out_count, DevStats* stats) {                                                                  \
-        shade_hero_batch(sc, h, ps, hp, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);           \
-    }
+        uint32_t* pq_out_count, DevStats* stats) PT_HERO_BODY
+#ifdef PT_TU_HERO
+#define PT_HERO_BODY { shade_hero_batch(sc, h, ps, hp, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats); }
+#else
+#define PT_HERO_BODY ;
+#endif
 PT_HERO_SHADE(k_shade_hero, )
 PT_HERO_SHADE(k_shade_hero_w2, __attribute__((amdgpu_waves_per_eu(2))))
 PT_HERO_SHADE(k_shade_hero_w4, __attribute__((amdgpu_waves_per_eu(4))))
 #undef PT_HERO_SHADE
+#undef PT_HERO_BODY
 
 // Film for SampledSpectrum samples: k_film's ordered per-pixel gather with a
 // 60-bin FilmTile contribSum (lane = bin), converted by ToXYZ at the merge
 // (film.h:121-161, film.cpp:117-130, spectrum.h:395-406).
 __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmConsts fc,
                                                   const int* __restrict__ pixslot, int p0, int np, int nsamp, int bx0,
-                                                  int by0, int bw, int bh, float4* accum) {
+                                                  int by0, int bw, int bh, float4* accum)
+#ifdef PT_TU_HERO
+{
     const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
     const int total = bw * bh;
@@ -802,6 +816,9 @@ __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmCo
         if (touched && lane == 0) accum[o] = acc;
     }
 }
+#else
+;
+#endif
 
 // SpatialLightDistribution::ComputeDistribution (lightdistrib.cpp:175-236)
 // for every voxel: 128 radical-inverse points, each light's Li.y() / pdf,
@@ -809,7 +826,9 @@ __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmCo
 // `ri` holds RadicalInverse(0..4, i) for i < 128; `light_y` each area
 // light's Lemit.y().
 __global__ void k_hero_spatial(DevScene sc, DevHero h, const float* __restrict__ ri, const float* __restrict__ light_y,
-                               float* dist) {
+                               float* dist)
+#ifdef PT_TU_HERO
+{
     const int nvox = h.nv0 * h.nv1 * h.nv2;
     const int nl = sc.n_lights;
     float tmp[kNS];
@@ -862,5 +881,8 @@ __global__ void k_hero_spatial(DevScene sc, DevHero h, const float* __restrict__
         d[2 * nl + 1] = funcInt;
     }
 }
+#else
+;
+#endif
 
 }  // namespace pt

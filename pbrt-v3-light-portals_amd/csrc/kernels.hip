@@ -9,6 +9,7 @@
 // mbcnt prefix).  k_film adds the finished samples to the film in sample
 // order (FilmTile::AddSample, film.h:121-161) by gathering over each pixel's
 // filter window -- deterministic, no float atomics.
+#pragma once
 #include "devfuncs.h"
 #include "kernels.h"
 #undef PT_FILE_ID
@@ -161,7 +162,9 @@ __device__ __forceinline__ void store_ray6(float* a, uint32_t n, uint32_t slot, 
 template <bool kLdsScene, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                        const uint32_t* __restrict__ rq_count, int* spill,
-                                                       DevStats* stats) {
+                                                       DevStats* stats)
+#ifdef PT_TU_TRACE
+{
     __shared__ int stk[kStackLds][kTraceBlock];
     extern __shared__ float4 lds_scene[];
     const float4* bnodes = sc.nodes;
@@ -202,6 +205,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
     }
     flush_stats(stats, ncl, nsh, nodes, prims);
 }
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // Persistent traversal with per-lane ray refill.  The same traversal as
@@ -238,7 +244,9 @@ template <bool kLdsScene, bool kSpill, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
                                                           int refill_min, int leaf_min, int stack_rows, int* spill,
-                                                          DevStats* stats) {
+                                                          DevStats* stats)
+#ifdef PT_TU_TRACE
+{
     // Dynamic LDS: [scene float4s if kLdsScene][stack].  With kSpill the
     // stack is kStackLds entries per lane plus a global spill; without, the
     // BVH is shallow enough that stack_rows entries per lane always suffice.
@@ -384,6 +392,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
     iters = wave_sum_u64(iters);
     if (lane == 0 && iters) atomicAdd(&stats->lane_iters, iters);
 }
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // k_trace_nb: k_trace_pt with the per-step control flow replaced by selects
@@ -394,7 +405,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
 template <bool kLdsScene, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
-                                                          int refill_min, int leaf_min, DevStats* stats) {
+                                                          int refill_min, int leaf_min, DevStats* stats)
+#ifdef PT_TU_TRACE
+{
     extern __shared__ float4 lds_dyn[];
     const float4* bnodes = sc.nodes;
     const float4* bprims = sc.prims;
@@ -526,6 +539,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
     const unsigned long long it = wave_sum_u64(iters);
     if (lane == 0 && it) atomicAdd(&stats->lane_iters, it);
 }
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
@@ -548,7 +564,9 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, float fx, float fy
 
 __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const int2* __restrict__ pix, int npix,
                                                 int s0, int nsamp, HaltonPixelConsts hp, uint32_t* rq,
-                                                uint32_t* pq) {
+                                                uint32_t* pq)
+#ifdef PT_TU_MISC
+{
     const uint32_t N = (uint32_t)ps.n;
     const uint32_t total = (uint32_t)npix * (uint32_t)nsamp;
     for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
@@ -581,6 +599,9 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
         pq[slot] = slot;
     }
 }
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // Shading
@@ -1246,7 +1267,9 @@ template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
                                                           const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                                           uint32_t* rq_out_count, uint32_t* pq_out,
-                                                          uint32_t* pq_out_count, DevStats* stats) {
+                                                          uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
     const uint32_t n = *pq_count;
     bool overflow = false;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
@@ -1266,6 +1289,9 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths 
     }
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
+#else
+;
+#endif
 
 // Register-budget variants of the shading kernel (occupancy vs spills), each
 // compiled for a scene-feature set kFt; render.hip picks one (PT_SHADE_VARIANT,
@@ -1274,34 +1300,37 @@ template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
                                                        const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                                        uint32_t* rq_out_count, uint32_t* pq_out,
-                                                       uint32_t* pq_out_count, DevStats* stats) {
+                                                       uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
     shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
+#else
+;
+#endif
 template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
     shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
+#else
+;
+#endif
 template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_w4(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
     shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
+#else
+;
+#endif
 
-template <int kFt>
-__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_shade_w5(
-    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
-    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
-}
-template <int kFt>
-__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_w6(
-    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats) {
-    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
-}
 
 // ----------------------------------------------------------------------------
 // Film: for every film pixel of the batch's region, rebuild each FilmTile's
@@ -1323,7 +1352,9 @@ __device__ __forceinline__ float lane_val(float v, int j) {
 }
 
 __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
-                                              int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum) {
+                                              int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum)
+#ifdef PT_TU_MISC
+{
     const uint32_t N = (uint32_t)ps.n;
     const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
@@ -1401,29 +1432,49 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
         if (touched && lane == 0) accum[o] = acc;
     }
 }
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // Test hooks (parity unit tests through the C ABI)
 // ----------------------------------------------------------------------------
-__global__ void k_debug_halton(DevScene sc, const uint32_t* idx, const int* dims, int n, float* out) {
+__global__ void k_debug_halton(DevScene sc, const uint32_t* idx, const int* dims, int n, float* out)
+#ifdef PT_TU_MISC
+{
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     out[i] = dims[i] < sc.max_dim ? halton_dim(sc, idx[i], dims[i]) : -1.f;
 }
-__global__ void k_debug_pixel_offset(DevScene sc, HaltonPixelConsts hp, const int2* pix, int n, uint32_t* out) {
+#else
+;
+#endif
+__global__ void k_debug_pixel_offset(DevScene sc, HaltonPixelConsts hp, const int2* pix, int n, uint32_t* out)
+#ifdef PT_TU_MISC
+{
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     out[i] = halton_pixel_offset(sc, pix[i].x, pix[i].y, hp.exp1, hp.scale0, hp.mi0, hp.mi1);
 }
-__global__ void k_debug_camera(DevScene sc, const float* film, int n, float* out) {
+#else
+;
+#endif
+__global__ void k_debug_camera(DevScene sc, const float* film, int n, float* out)
+#ifdef PT_TU_MISC
+{
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r = camera_ray(sc, film[2 * i], film[2 * i + 1], 0.5f, 0.5f);
     out[6 * i] = r.o.x; out[6 * i + 1] = r.o.y; out[6 * i + 2] = r.o.z;
     out[6 * i + 3] = r.d.x; out[6 * i + 4] = r.d.y; out[6 * i + 5] = r.d.z;
 }
+#else
+;
+#endif
 __global__ __launch_bounds__(kTraceBlock) void k_debug_trace(DevScene sc, const float* rays, int n, int any,
-                                                             int* spill, int* out_prim) {
+                                                             int* spill, int* out_prim)
+#ifdef PT_TU_MISC
+{
     __shared__ int stk[kStackLds][kTraceBlock];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1434,11 +1485,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_debug_trace(DevScene sc, const 
     out_prim[i] = any ? traverse<true>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b)
                       : traverse<false>(sc, sc.nodes, sc.prims, r, stk, sp, &a, &b);
 }
+#else
+;
+#endif
 
 // BSDF of scene material `mat` in the local frame n = (0,0,1): for each i,
 // in[8i..]: wo(3), wi(3), u0, u1 -> out[8i..]: f(3), pdf, sampled wi(3), sampled pdf
 // (sampled f replaces f when in wi is all zero).
-__global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float* out) {
+__global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float* out)
+#ifdef PT_TU_MISC
+{
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* a = in + 8 * i;
@@ -1462,5 +1518,8 @@ __global__ void k_debug_bsdf(DevScene sc, int mat, const float* in, int n, float
     o[0] = f.c[0]; o[1] = f.c[1]; o[2] = f.c[2]; o[3] = pdf;
     o[4] = ws.x; o[5] = ws.y; o[6] = ws.z; o[7] = spdf;
 }
+#else
+;
+#endif
 
 }  // namespace pt

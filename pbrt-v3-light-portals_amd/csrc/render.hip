@@ -15,8 +15,21 @@
 #include <vector>
 
 #include "host_common.h"
-#include "kernels.hip"
+// Kernel declarations (bodies compile in the tu_*.hip translation units, in
+// parallel); the PT_GUARDS diagnostic build compiles everything here so its
+// g_pt_guard symbol is the one every kernel writes.
+#ifdef PT_GUARDS
+#define PT_TU_TRACE 1
+#define PT_TU_SHADE 1
+#define PT_TU_MISC 1
+#define PT_TU_HERO 1
+#include "tu_trace.hip"
+#include "tu_shade.hip"
+#include "tu_misc.hip"
+#include "tu_hero.hip"
+#else
 #include "hero.hip"
+#endif
 
 namespace pt {
 
@@ -256,8 +269,6 @@ static ShadeKernel shade_kernel_ft(int variant) {
     switch (variant) {
         case 3: return k_shade_w3<kFt>;
         case 4: return k_shade_w4<kFt>;
-        case 5: return k_shade_w5<kFt>;
-        case 6: return k_shade_w6<kFt>;
         default: return k_shade<kFt>;
     }
 }
