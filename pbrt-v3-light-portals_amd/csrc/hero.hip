@@ -669,9 +669,10 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
                                                  DevStats* stats) {
     const uint32_t n = *pq_count;
     bool overflow = false;
+    PT_WAVEQ(wq);
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t rays[2];
+        uint32_t rays[3];
         uint32_t nrays = 0;
         bool keep = false;
         uint32_t slot = 0;
@@ -680,11 +681,9 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
             hero_step(sc, h, ps, hp, slot, rays, &nrays, &overflow);
             keep = (ps.st[slot] & (kStCont | kStNee)) != 0;
         }
-        const uint32_t pos = wave_reserve(rq_out_count, nrays);
-        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
-        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
-        if (keep) pq_out[ppos] = slot;
+        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
     }
+    wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
 

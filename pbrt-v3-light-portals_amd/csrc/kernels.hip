@@ -36,6 +36,65 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter, uint32_t cnt
     return base + prefix;
 }
 
+// Queue appends of one wave, staged in LDS across grid-stride iterations and
+// published with ONE packed 64-bit atomic per flush that reserves room in both
+// output queues (counts[2] = rays in the low word, counts[3] = paths in the
+// high word).  Same-address atomics serialise in one L2 channel: two per wave
+// per iteration bounded the shading kernels (doubling them doubled k_shade's
+// time), so a wave now flushes once per several hundred queue entries.
+#ifndef PT_WQR
+#define PT_WQR 448
+#define PT_WQP 192
+#endif
+constexpr uint32_t kWqRays = PT_WQR;   // >= 3 * 64: one iteration always fits after a flush
+constexpr uint32_t kWqPaths = PT_WQP;  // >= 64
+struct WaveQ {
+    uint32_t* r;       // LDS, kWqRays ray-queue entries
+    uint32_t* p;       // LDS, kWqPaths path-queue entries
+    uint32_t nr, np;   // fill levels (wave-uniform)
+};
+__device__ __forceinline__ void wq_flush(WaveQ& q, uint32_t* counts2, uint32_t* rq_out, uint32_t* pq_out) {
+    if ((q.nr | q.np) == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t lane = lane_id();
+    unsigned long long old = 0;
+    if (lane == 0)
+        old = atomicAdd((unsigned long long*)counts2, (unsigned long long)q.nr | ((unsigned long long)q.np << 32));
+    const uint32_t rb = (uint32_t)__shfl((int)(uint32_t)old, 0);
+    const uint32_t pb = (uint32_t)__shfl((int)(uint32_t)(old >> 32), 0);
+    for (uint32_t k = lane; k < q.nr; k += 64) rq_out[rb + k] = q.r[k];
+    for (uint32_t k = lane; k < q.np; k += 64) pq_out[pb + k] = q.p[k];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    q.nr = 0;
+    q.np = 0;
+}
+// Append nrays (0..3) ray entries and, if keep, the path slot.  Reached by
+// every lane of the wave together.
+__device__ __forceinline__ void wq_push(WaveQ& q, const uint32_t* rays, uint32_t nrays, bool keep, uint32_t slot,
+                                        uint32_t* counts2, uint32_t* rq_out, uint32_t* pq_out) {
+    const uint64_t b0 = __ballot((nrays & 1u) != 0);
+    const uint64_t b1 = __ballot((nrays & 2u) != 0);
+    const uint64_t bp = __ballot(keep);
+    const uint32_t lane = lane_id();
+    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t rtot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1);
+    const uint32_t ptot = (uint32_t)__popcll(bp);
+    if (q.nr + rtot > kWqRays || q.np + ptot > kWqPaths) wq_flush(q, counts2, rq_out, pq_out);
+    const uint32_t rpre = q.nr + (uint32_t)__popcll(b0 & lower) + 2u * (uint32_t)__popcll(b1 & lower);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k)
+        if (k < nrays) q.r[rpre + k] = rays[k];
+    if (keep) q.p[q.np + (uint32_t)__popcll(bp & lower)] = slot;
+    q.nr += rtot;
+    q.np += ptot;
+}
+#define PT_WAVEQ(q)                                                   \
+    __shared__ uint32_t wq_r_[kShadeBlock / 64][kWqRays];             \
+    __shared__ uint32_t wq_p_[kShadeBlock / 64][kWqPaths];            \
+    WaveQ q{wq_r_[threadIdx.x / 64], wq_p_[threadIdx.x / 64], 0u, 0u}
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
@@ -991,6 +1050,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
                                             DevStats* stats) {
     const uint32_t n = *pq_count;
     bool overflow = false;
+    PT_WAVEQ(wq);
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         uint32_t rays[3];
@@ -1001,11 +1061,9 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
             slot = pq[i];
             shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
         }
-        const uint32_t pos = wave_reserve(rq_out_count, nrays);
-        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
-        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
-        if (keep) pq_out[ppos] = slot;
+        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
     }
+    wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
 
@@ -1272,6 +1330,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths 
 {
     const uint32_t n = *pq_count;
     bool overflow = false;
+    PT_WAVEQ(wq);
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         uint32_t rays[3];
@@ -1282,11 +1341,9 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths 
             slot = pq[i];
             shade_dl<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
         }
-        const uint32_t pos = wave_reserve(rq_out_count, nrays);
-        for (uint32_t k = 0; k < nrays; ++k) rq_out[pos + k] = rays[k];
-        const uint32_t ppos = wave_reserve(pq_out_count, keep ? 1u : 0u);
-        if (keep) pq_out[ppos] = slot;
+        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
     }
+    wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
 }
 #else
