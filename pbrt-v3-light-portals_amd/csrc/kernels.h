@@ -6,7 +6,8 @@
 
 namespace pt {
 
-constexpr int kTraceBlock = 128;  // 2 waves; LDS stack = kStackLds * 128 * 4 B
+constexpr int kTraceBlock = 128;
+constexpr uint32_t kTraceChunk = 512;  // ray-queue entries a k_trace_nb wave takes per atomic  // 2 waves; LDS stack = kStackLds * 128 * 4 B
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
 constexpr int kMaxPortals = 64;

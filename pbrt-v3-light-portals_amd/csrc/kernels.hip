@@ -484,7 +484,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
     const uint32_t lane = lane_id();
     const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
-    bool active = false, exhausted = false;
+    bool active = false, exhausted = false, drained = false;
+    // The wave takes queue entries kTraceChunk at a time (one atomic) and
+    // hands them to its idle lanes from that private chunk, so frequent partial
+    // refills do not each hit the one shared counter.
+    uint32_t qn = 0, qe = 0;
     uint32_t slot = 0, kind = 0;
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
     V3 inv = v3(0, 0, 0);
@@ -496,13 +500,21 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if (nidle >= (uint32_t)refill_min || nidle == 64u) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(fetch, nidle);
-                base = (uint32_t)__shfl((int)base, 0);
-                if (base + nidle >= n) exhausted = true;
+                if (qn >= qe && !drained) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
+                    base = (uint32_t)__shfl((int)base, 0);
+                    qn = base < n ? base : n;
+                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
+                    drained = base + kTraceChunk >= n;
+                }
+                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
+                const uint32_t k = (uint32_t)__popcll(idle & lower);
+                const uint32_t i = qn + k;
+                qn += take;
+                if (drained && qn >= qe) exhausted = true;
                 if (!active) {
-                    const uint32_t i = base + (uint32_t)__popcll(idle & lower);
-                    if (i < n) {
+                    if (k < take) {
                         const uint32_t e = rq[i];
                         slot = e >> 2;
                         kind = e & 3u;
