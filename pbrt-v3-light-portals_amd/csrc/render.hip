@@ -229,7 +229,7 @@ struct pt_scene {
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     int hero_waves = 4;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4)
-    int shade_variant = 4;       // 0: compiler register budget, 3/4: forced waves per SIMD
+    int shade_variant = 0;       // 0: compiler register budget (no scratch), 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
