@@ -7,11 +7,13 @@ closed Cornell interior lit by an aaplane emitter behind one axis-aligned
 portal, PathIntegrator maxdepth 5, 1920x1080, Halton 256 spp, box filter,
 portal strategy "portal".  Synthetic scene (no downloads).
 
-A step = one full 1920x1080 x 256-spp frame per rank.  Ranks shard the
-camera-sample index space (rank r renders samples [256 r, 256 r + 256) of
-every pixel: weak scaling, independent units, no data-path collective); the
-film accumulators are summed once per step with an RCCL reduce to rank 0
-(the only collective, inside the timed region).
+A step = one full 1920x1080 x 256-spp frame.  With N ranks (one process per
+GPU) the 16x16 tiles are dealt round-robin (rank r renders tiles t % N == r:
+strong scaling, the same frame at every N, independent units, no data-path
+collective); the device films are summed once per step onto rank 0 with one
+RCCL ncclReduce issued by the library (pt_render_frame_dist, the only
+collective, inside the timed region).  --shard samples is the opt-in weak
+scaling mode (rank r renders sample indices [r*spp, (r+1)*spp)).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -59,7 +61,7 @@ def parse():
     ap.add_argument("--res", default="", help="override WxH")
     ap.add_argument("--strategy", default="", help="override portal strategy")
     ap.add_argument("--batch-slots", type=int, default=0)
-    ap.add_argument("--shard", default="samples", help="samples (weak) | samples-split | tiles (strong)")
+    ap.add_argument("--shard", default="tiles", help="tiles (strong, default) | samples-split (strong) | samples (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -151,9 +153,17 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     my = shardmod.plan(rank, world, spp, args.shard)
     render = shardmod.device_renderer(sc, accum.data_ptr(), stream)
+    comm = None
+    if world > 1:  # the library's own RCCL communicator (id handed over by torch.distributed)
+        uid = [ptgpu.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = ptgpu.Comm(world, rank, uid[0])
 
     def step():
-        return shardmod.render_frame(my, render, accum, shardmod.reduce_to_root)
+        if comm is not None and args.shard == "tiles":
+            return comm.render_frame(sc, accum.data_ptr(), stream)
+        return shardmod.render_frame(my, render, accum,
+                                     (lambda a: comm.reduce(sc, a.data_ptr(), 0, stream)) if comm else None)
 
     for _ in range(args.warmup):
         step()
@@ -200,7 +210,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak" if args.shard == "samples" else "strong",
+            "scaling": shardmod.scaling(args.shard),
             "vs_baseline": None,
             "dtype": "f32",
             "data": cdata,
@@ -220,6 +230,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spath, args.cpu_seconds)
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
     try:

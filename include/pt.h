@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4
+#define PT_ABI_VERSION 5
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -285,8 +285,17 @@ typedef struct pt_scene pt_scene;
 int pt_abi_version(void);
 const char* pt_last_error(void);
 
-/* Select the HIP device for this host thread. */
-pt_status pt_init(int device);
+/* The devices this process renders on: device_ids[0..count)
+ * (NULL: 0..count-1).  Scenes created afterwards hold one replica per device
+ * (the BVH is built once on the host) and pt_render deals the 16x16 tiles
+ * round-robin over them, one host thread per device (the reference's
+ * ParallelFor2D over tiles, integrator.cpp:533-538), summing the device films
+ * on device_ids[0] in device order (Film::MergeFilmTile, film.cpp:117-130).
+ * count 1 is the single-device path; without pt_init the calling thread's
+ * current HIP device is used. */
+pt_status pt_init(int device_count, const int32_t* device_ids);
+/* Forget the device list (scenes keep their devices until destroyed). */
+pt_status pt_shutdown(void);
 
 /* Build the SAH BVH on the host (BVHAccel, bvh.cpp:236-402) and upload the
  * flattened scene to device memory. */
@@ -298,9 +307,12 @@ void pt_scene_destroy(pt_scene* scene);
 pt_status pt_scene_bvh(const pt_scene* scene, int32_t* n_nodes, void* nodes32,
                        int32_t* n_prims, int32_t* prim_order);
 
-/* Host-only BVH build (no device needed): same nodes as pt_scene_bvh. */
-pt_status pt_build_bvh_host(const pt_scene_desc* desc, int32_t* n_nodes, void* nodes32,
-                            int32_t* prim_order, int32_t cap);
+/* Host-only BVH build (no device needed): same nodes as pt_scene_bvh.
+ * n_nodes / n_prims receive the counts (pass NULL buffers to query them);
+ * a buffer smaller than its count (node_cap nodes, prim_cap entries) is
+ * PT_ERR_INVALID_ARG. */
+pt_status pt_build_bvh_host(const pt_scene_desc* desc, int32_t* n_nodes, void* nodes32, int32_t node_cap,
+                            int32_t* n_prims, int32_t* prim_order, int32_t prim_cap);
 
 /* Render the whole sample-bound region serially on this device and write the
  * final RGB image (croppedPixelBounds, 3 floats per pixel, WriteImage
@@ -325,6 +337,21 @@ pt_status pt_render_range(pt_scene* scene, int tile_offset, int tile_stride,
                           int sample_begin, int sample_end, float* d_accum,
                           void* stream, pt_stats* stats);
 
+/* ---- multi-process (one process per GPU): RCCL over xGMI ----
+ * Rank 0 calls pt_comm_unique_id and hands the PT_COMM_ID_BYTES to every rank
+ * (any launcher channel); each rank selects its GPU (pt_init(1, &id)) and calls
+ * pt_comm_create.  pt_render_frame_dist renders the tiles t % nranks == rank
+ * into d_accum (zeroed by the call) on `stream` and sums the films onto rank 0
+ * with one ncclReduce -- the frame's only collective. */
+#define PT_COMM_ID_BYTES 128
+typedef struct pt_comm pt_comm;
+pt_status pt_comm_unique_id(uint8_t* id_out);
+pt_status pt_comm_create(int nranks, int rank, const uint8_t* id, pt_comm** out);
+void pt_comm_destroy(pt_comm* comm);
+/* ncclReduce(sum) of a device film (4 floats per cropped pixel) to `root`. */
+pt_status pt_film_reduce(pt_comm* comm, const pt_scene* scene, float* d_accum, int root, void* stream);
+pt_status pt_render_frame_dist(pt_scene* scene, pt_comm* comm, float* d_accum, void* stream, pt_stats* stats);
+
 /* Resolve an accumulation buffer (host memory, 4 floats per pixel: XYZ sum +
  * weight sum) into the final RGB image exactly as Film::WriteImage does
  * (film.cpp:169-211). */
@@ -346,8 +373,10 @@ pt_status pt_render_range_accum(pt_scene* scene, int tile_offset, int tile_strid
                                 int sample_begin, int sample_end, float* accum_out,
                                 pt_stats* stats);
 
-/* Number of in-flight paths per wavefront batch (default 8M).  Memory for
- * path state is ~230 bytes per slot. */
+/* Number of in-flight paths per wavefront batch (default 64M; 8M for the
+ * hero integrators).  Memory for path state is ~230 bytes per slot (~1.2 KB
+ * for the hero integrators).  Batches beyond the 32-bit path-state indexing
+ * limit (~252M slots; ~70M for hero scenes) are PT_ERR_INVALID_ARG. */
 pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
 
 /* Number of cropped pixels (rgb_out holds 3x this many floats). */

@@ -1,5 +1,5 @@
 // ptrender.cpp -- pbrt-style command line (src/main/pbrt.cpp:43-173 subset)
-// on top of the C ABI: ptrender [--outfile f] [--device N] [--quiet]
+// on top of the C ABI: ptrender [--outfile f] [--device N | --devices a,b,..] [--quiet]
 // [--stats] scene.pbrt.  The image goes to the Film's "filename" (default
 // pbrt.exr) unless --outfile overrides it (film.cpp:213-225); the suffix
 // picks EXR / PFM / PNG / TGA (Film::WriteImage -> WriteImage, imageio.cpp:81-122).
@@ -12,17 +12,26 @@
 #include "../../include/pt.h"
 
 static void usage() {
-    std::fprintf(stderr, "usage: ptrender [--outfile file.{exr,pfm,png,tga}] [--device N] [--quiet] [--stats] scene.pbrt\n");
+    std::fprintf(stderr, "usage: ptrender [--outfile file.{exr,pfm,png,tga}] [--device N | --devices a,b,...] [--quiet] [--stats] scene.pbrt\n");
     std::exit(1);
 }
 
 int main(int argc, char** argv) {
     std::string out, scene;
-    int device = 0;
+    std::vector<int32_t> devices{0};
     bool quiet = false, stats = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--outfile") && i + 1 < argc) out = argv[++i];
-        else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) devices = {std::atoi(argv[++i])};
+        else if (!std::strcmp(argv[i], "--devices") && i + 1 < argc) {  // one process, tiles over these GPUs
+            devices.clear();
+            for (const char* p = argv[++i]; *p;) {
+                devices.push_back((int32_t)std::strtol(p, (char**)&p, 10));
+                if (*p == ',') ++p;
+                else if (*p) usage();
+            }
+            if (devices.empty()) usage();
+        }
         else if (!std::strcmp(argv[i], "--quiet")) quiet = true;
         else if (!std::strcmp(argv[i], "--stats")) stats = true;
         else if (argv[i][0] == '-') usage();
@@ -34,7 +43,7 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "ptrender: %s\n", pt_last_error());
         return 1;
     }
-    if (pt_init(device) != PT_OK) {
+    if (pt_init((int)devices.size(), devices.data()) != PT_OK) {
         std::fprintf(stderr, "ptrender: %s\n", pt_last_error());
         return 1;
     }

@@ -11,8 +11,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "host_common.h"
 // Kernel declarations (bodies compile in the tu_*.hip translation units, in
@@ -238,6 +242,16 @@ struct pt_scene {
     int leaf_min = 24;           // lanes parked at leaves that trigger a primitive-test step
     int trace_spill = 1;         // BVH deeper than the LDS stack: keep the global spill path
     int stack_rows = pt::kStackLds;  // LDS stack entries per lane in k_trace_pt
+    // pt_init(n > 1, ids): one replica per further device of the process
+    // (same scene, same host-built BVH), rendered by one host thread each
+    std::vector<std::unique_ptr<pt_scene>> replicas;
+    std::vector<int> devices;  // ids[0..n) the scene was created for (primary first)
+};
+
+// Multi-process communicator (pt_comm_create): RCCL over the GPUs of the job
+struct pt_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
 };
 
 namespace pt {
@@ -490,7 +504,7 @@ static void build_hero(pt_scene* s, const pt_scene_desc* d, const std::vector<De
     s->hero = true;
 }
 
-static void build_scene(pt_scene* s, const pt_scene_desc* d) {
+static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh_src) {
     if (!d) throw PtError(PT_ERR_INVALID_ARG, "null scene description");
     if (d->n_prims < 0 || d->n_triangles < 0 || d->n_planes < 0 || d->n_lights < 0 || d->n_materials < 0)
         throw PtError(PT_ERR_INVALID_ARG, "negative counts in scene description");
@@ -554,8 +568,12 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
     if (d->integrator.max_depth < 0 || d->integrator.max_depth > 250)
         throw PtError(PT_ERR_UNSUPPORTED, "maxdepth must be in [0, 250]");
 
-    // ---- BVH (host build, reference order) ----
-    build_bvh(d, &s->host_nodes, &s->host_prim_order);
+    // ---- BVH (host build, reference order; replicas reuse the primary's) ----
+    if (bvh_src) {
+        s->host_nodes = bvh_src->host_nodes;
+        s->host_prim_order = bvh_src->host_prim_order;
+    } else
+        build_bvh(d, &s->host_nodes, &s->host_prim_order);
     std::vector<float4> nodes(2 * s->host_nodes.size());
     for (size_t i = 0; i < s->host_nodes.size(); ++i) {
         const LinearNode& n = s->host_nodes[i];
@@ -895,6 +913,14 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d) {
         throw PtError(PT_ERR_INVALID_ARG, "hero integrators need a spectral (SampledSpectrum) scene description");
 }
 
+// Largest batch the device indexing supports: path-state fields are
+// addressed as field * N + slot in 32-bit arithmetic (kNee payload floats;
+// the hero integrators' 60-bin SoA), so (fields + 1) * N must stay below 2^32.
+static uint64_t slot_limit(const pt_scene* s) {
+    const uint64_t fields = s->hero ? (uint64_t)kNSpec + 1 : (uint64_t)kNee + 1;
+    return 0xffffffffull / fields;
+}
+
 // Pixels of tiles t with t % stride == offset, tile order then scan order
 // (integrator.cpp:533-560), restricted to the integrator's pixelBounds.
 // tiles receives, per selected non-empty tile, its first index into pix and
@@ -995,6 +1021,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         groups.push_back(g);
         i = j;
     }
+    if (max_slots > slot_limit(s)) throw PtError(PT_ERR_INVALID_ARG, "batch exceeds the path-state indexing limit");
     DBuf<int2> dpix;
     dpix.upload(pix);
     DBuf<int> dslot;
@@ -1238,6 +1265,136 @@ static void require_device() {
     if (e != hipSuccess || n == 0) throw PtError(PT_ERR_DEVICE, "no HIP device available (the product has no CPU fallback)");
 }
 
+#define NCCLCHK(x)                                                                                      \
+    do {                                                                                                \
+        ncclResult_t r_ = (x);                                                                          \
+        if (r_ != ncclSuccess) throw PtError(PT_ERR_DEVICE, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// The devices of this process (pt_init); empty: the calling thread's current device.
+static std::vector<int> g_devices;
+static std::mutex g_devices_mu;
+
+// Deepest traversal stack the flattened BVH can need: interior nodes on the
+// longest root-to-leaf path (each pushes one entry).
+static int bvh_stack_bound(const std::vector<LinearNode>& nodes) {
+    if (nodes.empty()) return 0;
+    int best = 0;
+    std::vector<std::pair<int, int>> todo{{0, 0}};
+    while (!todo.empty()) {
+        auto [i, d] = todo.back();
+        todo.pop_back();
+        if (i < 0 || i >= (int)nodes.size()) continue;
+        if (nodes[i].nprims > 0) { best = std::max(best, d); continue; }
+        todo.push_back({i + 1, d + 1});
+        todo.push_back({nodes[i].offset, d + 1});
+    }
+    return best;
+}
+
+// One device's copy of the scene: build (or copy the BVH of bvh_src),
+// upload, and pick the kernel variants for it.
+static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc* desc, const pt_scene* bvh_src) {
+    HIPCHK(hipSetDevice(device));
+    std::unique_ptr<pt_scene> s(new pt_scene);
+    s->device = device;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, s->device));
+    s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    s->features = scene_features(desc);
+    if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
+    build_scene(s.get(), desc, bvh_src);
+    const int sbound = bvh_stack_bound(s->host_nodes);
+    s->trace_spill = sbound > kStackLds;
+    s->stack_rows = s->trace_spill ? kStackLds : std::max(1, sbound);
+    if (const char* t = std::getenv("PT_STACK_ROWS")) {  // test hook: force the spill path
+        s->stack_rows = std::max(1, std::min(kStackLds, std::atoi(t)));
+        s->trace_spill = sbound > s->stack_rows;
+    }
+    // kernel variants: LDS-resident BVH for small scenes (PT_TRACE_LDS=0 disables),
+    // shading register budget (PT_SHADE_VARIANT=3|4)
+    const size_t scene_bytes = (2 * (size_t)s->dev.n_nodes + 3 * (size_t)s->dev.n_prims) * sizeof(float4);
+    const char* e = std::getenv("PT_TRACE_LDS");
+    s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
+                             ? scene_bytes : 0;
+    if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
+    const char* v = std::getenv("PT_SHADE_VARIANT");
+    if (v) s->shade_variant = std::atoi(v);
+    s->has_spheres = (s->features & kFtSphere) != 0;
+    if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
+    if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
+    if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
+    return s;
+}
+
+__global__ void k_film_add(float4* __restrict__ dst, const float4* __restrict__ src, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 a = dst[i], b = src[i];
+        dst[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+}
+
+static void add_stats(RenderResult* a, const RenderResult& b) {
+    a->st.closest += b.st.closest; a->st.shadow += b.st.shadow; a->st.nodes += b.st.nodes; a->st.prims += b.st.prims;
+    a->st.dim_overflow += b.st.dim_overflow; a->st.lane_iters += b.st.lane_iters; a->st.lane_steps += b.st.lane_steps;
+    a->samples += b.samples;
+    a->launches += b.launches;
+    a->trace_ms += b.trace_ms;
+    a->render_ms = std::max(a->render_ms, b.render_ms);
+}
+
+// The whole frame on every device of the scene (SamplerIntegrator::Render
+// with the tile loop dealt round-robin over the devices, t % n == k), one host
+// thread per device, each into its own device film; the films are summed on
+// the primary device in device order (peer copies over xGMI) -- a fixed order,
+// so the result does not depend on thread timing.
+static RenderResult render_all_devices(pt_scene* s, float4* d_accum0) {
+    const int nd = 1 + (int)s->replicas.size();
+    std::vector<pt_scene*> sc(nd);
+    sc[0] = s;
+    for (int k = 1; k < nd; ++k) sc[k] = s->replicas[k - 1].get();
+    const size_t np = (size_t)s->fr.width() * s->fr.height();
+    std::vector<std::unique_ptr<DBuf<float4>>> films(nd);
+    std::vector<RenderResult> res(nd);
+    std::vector<std::exception_ptr> err(nd);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nd; ++k)
+        th.emplace_back([&, k] {
+            try {
+                HIPCHK(hipSetDevice(sc[k]->device));
+                float4* film = d_accum0;
+                if (k > 0) {
+                    films[k].reset(new DBuf<float4>);
+                    films[k]->alloc(np);
+                    film = films[k]->p;
+                    HIPCHK(hipMemset(film, 0, np * sizeof(float4)));
+                }
+                res[k] = render_tiles(sc[k], k, nd, 0, sc[k]->spp, film, nullptr);
+            } catch (...) {
+                err[k] = std::current_exception();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    HIPCHK(hipSetDevice(s->device));
+    RenderResult out = res[0];
+    if (nd > 1) {
+        DBuf<float4> tmp;
+        tmp.alloc(np);
+        for (int k = 1; k < nd; ++k) {
+            HIPCHK(hipMemcpyPeer(tmp.p, s->device, films[k]->p, sc[k]->device, np * sizeof(float4)));
+            hipLaunchKernelGGL(k_film_add, dim3(std::max(1, std::min(ceil_div((long)np, 256), 4096))), dim3(256), 0, 0,
+                               d_accum0, tmp.p, np);
+            HIPCHK(hipGetLastError());
+            add_stats(&out, res[k]);
+        }
+        HIPCHK(hipDeviceSynchronize());
+    }
+    return out;
+}
+
 }  // namespace pt
 
 using namespace pt;
@@ -1263,63 +1420,98 @@ void pt_host_scene_free(pt_host_scene* hs) {
     if (hs) host_scene_free((pt_host_scene_impl*)hs);
 }
 
-pt_status pt_init(int device) {
+pt_status pt_init(int device_count, const int32_t* device_ids) {
     return guarded([&] {
         require_device();
-        HIPCHK(hipSetDevice(device));
+        int n = 0;
+        HIPCHK(hipGetDeviceCount(&n));
+        if (device_count < 1) throw PtError(PT_ERR_INVALID_ARG, "device_count must be >= 1");
+        std::vector<int> ids((size_t)device_count);
+        for (int k = 0; k < device_count; ++k) {
+            ids[k] = device_ids ? device_ids[k] : k;
+            if (ids[k] < 0 || ids[k] >= n) throw PtError(PT_ERR_INVALID_ARG, "device id out of range");
+        }
+        HIPCHK(hipSetDevice(ids[0]));
+        std::lock_guard<std::mutex> lk(g_devices_mu);
+        g_devices = ids;
     });
 }
 
-// Deepest traversal stack the flattened BVH can need: interior nodes on the
-// longest root-to-leaf path (each pushes one entry).
-static int bvh_stack_bound(const std::vector<LinearNode>& nodes) {
-    if (nodes.empty()) return 0;
-    int best = 0;
-    std::vector<std::pair<int, int>> todo{{0, 0}};
-    while (!todo.empty()) {
-        auto [i, d] = todo.back();
-        todo.pop_back();
-        if (i < 0 || i >= (int)nodes.size()) continue;
-        if (nodes[i].nprims > 0) { best = std::max(best, d); continue; }
-        todo.push_back({i + 1, d + 1});
-        todo.push_back({nodes[i].offset, d + 1});
-    }
-    return best;
+pt_status pt_shutdown(void) {
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(g_devices_mu);
+        g_devices.clear();
+    });
+}
+
+pt_status pt_comm_unique_id(uint8_t* id_out) {
+    return guarded([&] {
+        if (!id_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        static_assert(sizeof(ncclUniqueId) == PT_COMM_ID_BYTES, "ncclUniqueId size");
+        ncclUniqueId id;
+        NCCLCHK(ncclGetUniqueId(&id));
+        std::memcpy(id_out, &id, sizeof id);
+    });
+}
+
+pt_status pt_comm_create(int nranks, int rank, const uint8_t* id, pt_comm** out) {
+    return guarded([&] {
+        if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        require_device();
+        std::unique_ptr<pt_comm> c(new pt_comm);
+        HIPCHK(hipGetDevice(&c->device));
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof uid);
+        NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+        c->nranks = nranks;
+        c->rank = rank;
+        *out = c.release();
+    });
+}
+
+void pt_comm_destroy(pt_comm* comm) {
+    if (!comm) return;
+    if (comm->comm) (void)ncclCommDestroy(comm->comm);
+    delete comm;
+}
+
+pt_status pt_film_reduce(pt_comm* comm, const pt_scene* s, float* d_accum, int root, void* stream) {
+    return guarded([&] {
+        if (!comm || !s || !d_accum || root < 0 || root >= comm->nranks) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        const size_t n = 4 * (size_t)s->fr.width() * s->fr.height();
+        NCCLCHK(ncclReduce(d_accum, d_accum, n, ncclFloat, ncclSum, root, comm->comm, (hipStream_t)stream));
+    });
+}
+
+pt_status pt_render_frame_dist(pt_scene* s, pt_comm* comm, float* d_accum, void* stream, pt_stats* stats) {
+    return guarded([&] {
+        if (!s || !comm || !d_accum) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        const size_t np = (size_t)s->fr.width() * s->fr.height();
+        HIPCHK(hipMemsetAsync(d_accum, 0, np * sizeof(float4), (hipStream_t)stream));
+        RenderResult r = render_tiles(s, comm->rank, comm->nranks, 0, s->spp, (float4*)d_accum, (hipStream_t)stream);
+        NCCLCHK(ncclReduce(d_accum, d_accum, 4 * np, ncclFloat, ncclSum, 0, comm->comm, (hipStream_t)stream));
+        fill_stats(r, stats);
+    });
 }
 
 pt_status pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     return guarded([&] {
         if (!out) throw PtError(PT_ERR_INVALID_ARG, "null out");
         require_device();
-        std::unique_ptr<pt_scene> s(new pt_scene);
-        HIPCHK(hipGetDevice(&s->device));
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, s->device));
-        s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-        s->features = scene_features(desc);
-        if (const char* t = std::getenv("PT_SHADE_FEATURES")) s->features |= std::atoi(t) & kFtAll;
-        build_scene(s.get(), desc);
-        const int sbound = bvh_stack_bound(s->host_nodes);
-        s->trace_spill = sbound > kStackLds;
-        s->stack_rows = s->trace_spill ? kStackLds : std::max(1, sbound);
-        if (const char* t = std::getenv("PT_STACK_ROWS")) {  // test hook: force the spill path
-            s->stack_rows = std::max(1, std::min(kStackLds, std::atoi(t)));
-            s->trace_spill = sbound > s->stack_rows;
+        std::vector<int> ids;
+        {
+            std::lock_guard<std::mutex> lk(g_devices_mu);
+            ids = g_devices;
         }
-        // kernel variants: LDS-resident BVH for small scenes (PT_TRACE_LDS=0 disables),
-        // shading register budget (PT_SHADE_VARIANT=3|4)
-        const size_t scene_bytes = (2 * (size_t)s->dev.n_nodes + 3 * (size_t)s->dev.n_prims) * sizeof(float4);
-        const char* e = std::getenv("PT_TRACE_LDS");
-        s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
-                                 ? scene_bytes : 0;
-        if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
-        const char* v = std::getenv("PT_SHADE_VARIANT");
-        if (v) s->shade_variant = std::atoi(v);
-        s->has_spheres = (s->features & kFtSphere) != 0;
-        if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
-        if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
-        if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
-        if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
+        if (ids.empty()) {
+            int d = 0;
+            HIPCHK(hipGetDevice(&d));
+            ids.push_back(d);
+        }
+        std::unique_ptr<pt_scene> s = create_scene_on(ids[0], desc, nullptr);
+        for (size_t k = 1; k < ids.size(); ++k) s->replicas.push_back(create_scene_on(ids[k], desc, s.get()));
+        HIPCHK(hipSetDevice(ids[0]));
+        s->devices = ids;
         *out = s.release();
     });
 }
@@ -1337,17 +1529,23 @@ pt_status pt_scene_bvh(const pt_scene* s, int32_t* n_nodes, void* nodes32, int32
     });
 }
 
-pt_status pt_build_bvh_host(const pt_scene_desc* d, int32_t* n_nodes, void* nodes32, int32_t* prim_order,
-                            int32_t cap) {
+pt_status pt_build_bvh_host(const pt_scene_desc* d, int32_t* n_nodes, void* nodes32, int32_t node_cap,
+                            int32_t* n_prims, int32_t* prim_order, int32_t prim_cap) {
     return guarded([&] {
         if (!d || !n_nodes) throw PtError(PT_ERR_INVALID_ARG, "null argument");
         std::vector<LinearNode> nodes;
         std::vector<int> order;
         build_bvh(d, &nodes, &order);
         *n_nodes = (int32_t)nodes.size();
-        if (nodes32 && (int32_t)nodes.size() <= cap) std::memcpy(nodes32, nodes.data(), nodes.size() * sizeof(LinearNode));
-        if (prim_order && (int32_t)order.size() <= cap)
+        if (n_prims) *n_prims = (int32_t)order.size();
+        if (nodes32) {
+            if ((int64_t)nodes.size() > node_cap) throw PtError(PT_ERR_INVALID_ARG, "node buffer too small");
+            std::memcpy(nodes32, nodes.data(), nodes.size() * sizeof(LinearNode));
+        }
+        if (prim_order) {
+            if ((int64_t)order.size() > prim_cap) throw PtError(PT_ERR_INVALID_ARG, "prim order buffer too small");
             for (size_t i = 0; i < order.size(); ++i) prim_order[i] = order[i];
+        }
     });
 }
 
@@ -1434,10 +1632,12 @@ pt_status pt_render(pt_scene* s, float* rgb_out, pt_stats* stats) {
     return guarded([&] {
         if (!s || !rgb_out) throw PtError(PT_ERR_INVALID_ARG, "null argument");
         size_t np = (size_t)s->fr.width() * s->fr.height();
+        HIPCHK(hipSetDevice(s->device));
         DBuf<float4> acc;
         acc.alloc(np);
         HIPCHK(hipMemset(acc.p, 0, np * sizeof(float4)));
-        RenderResult r = render_tiles(s, 0, 1, 0, s->spp, acc.p, nullptr);
+        RenderResult r = s->replicas.empty() ? render_tiles(s, 0, 1, 0, s->spp, acc.p, nullptr)
+                                             : render_all_devices(s, acc.p);
         std::vector<float> h(4 * np);
         HIPCHK(hipMemcpy(h.data(), acc.p, np * sizeof(float4), hipMemcpyDeviceToHost));
         resolve(s, h.data(), rgb_out);
@@ -1448,6 +1648,9 @@ pt_status pt_render(pt_scene* s, float* rgb_out, pt_stats* stats) {
 pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
     return guarded([&] {
         if (!s || slots <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        if ((uint64_t)slots > slot_limit(s))
+            throw PtError(PT_ERR_INVALID_ARG, "batch slots exceed the 32-bit path-state indexing limit (" +
+                                                  std::to_string(slot_limit(s)) + ")");
         s->target_slots = (size_t)slots;
     });
 }

@@ -62,12 +62,19 @@ def lib() -> ctypes.CDLL:
     L.pt_host_scene_desc.restype = vp
     L.pt_host_scene_free.argtypes = [vp]
     L.pt_host_scene_free.restype = None
-    L.pt_init.argtypes = [ctypes.c_int]
+    L.pt_init.argtypes = [ctypes.c_int, ctypes.POINTER(i32)]
+    L.pt_shutdown.argtypes = []
+    L.pt_comm_unique_id.argtypes = [vp]
+    L.pt_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.pt_comm_destroy.argtypes = [vp]
+    L.pt_comm_destroy.restype = None
+    L.pt_film_reduce.argtypes = [vp, vp, vp, ctypes.c_int, vp]
+    L.pt_render_frame_dist.argtypes = [vp, vp, vp, vp, ctypes.POINTER(pt_stats)]
     L.pt_scene_create.argtypes = [vp, ctypes.POINTER(vp)]
     L.pt_scene_destroy.argtypes = [vp]
     L.pt_scene_destroy.restype = None
     L.pt_scene_bvh.argtypes = [vp, ctypes.POINTER(i32), vp, ctypes.POINTER(i32), vp]
-    L.pt_build_bvh_host.argtypes = [vp, ctypes.POINTER(i32), vp, vp, i32]
+    L.pt_build_bvh_host.argtypes = [vp, ctypes.POINTER(i32), vp, i32, ctypes.POINTER(i32), vp, i32]
     L.pt_film_size.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_render.argtypes = [vp, f32p, ctypes.POINTER(pt_stats)]
     L.pt_render_accum.argtypes = [vp, ctypes.c_int, ctypes.c_int, f32p, ctypes.POINTER(pt_stats)]
@@ -207,14 +214,13 @@ class HostScene:
 
     def bvh(self) -> Tuple[np.ndarray, np.ndarray]:
         """Host SAH BVH (bvh.cpp): (n, 8) uint32 LinearBVHNode images, prim order."""
-        n = ctypes.c_int32()
-        _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), None, None, 0))
+        n, m = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), None, 0, ctypes.byref(m), None, 0))
         nodes = np.zeros((n.value, 8), np.uint32)
-        # prim count <= 2 * nodes
-        order = np.zeros(max(1, 2 * n.value), np.int32)
-        _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), nodes.ctypes.data, order.ctypes.data,
-                                       int(2 * n.value)))
-        return nodes, order
+        order = np.zeros(max(1, m.value), np.int32)
+        _check(lib().pt_build_bvh_host(self.desc, ctypes.byref(n), nodes.ctypes.data, n.value, ctypes.byref(m),
+                                       order.ctypes.data, m.value))
+        return nodes, order[:m.value]
 
     def materials(self) -> list:
         """The scene's pt_material records (copies) -- host only."""
@@ -243,6 +249,10 @@ class HostScene:
         w, h = ctypes.c_int32(), ctypes.c_int32()
         _check(lib().pt_film_size_host(self.desc, ctypes.byref(w), ctypes.byref(h)))
         return w.value, h.value
+
+    def spp(self) -> int:
+        """Sampler "pixelsamples" of the scene -- host only."""
+        return ctypes.cast(ctypes.c_void_p(self.desc), ctypes.POINTER(pt_scene_desc)).contents.sampler.spp
 
     @property
     def film_filename(self) -> str:
@@ -281,9 +291,15 @@ class HostScene:
 class Scene:
     """Device scene (pt_scene_create): BVH + SoA buffers resident in HBM."""
 
-    def __init__(self, host: HostScene, device: int = 0, batch_slots: Optional[int] = None):
+    def __init__(self, host: HostScene, device: int = 0, batch_slots: Optional[int] = None,
+                 devices: Optional[list] = None):
+        """device: the GPU of this process; devices: several GPUs of this
+        process (pt_init(n, ids): one scene replica per device, pt_render deals
+        the tiles over them)."""
         self.host = host
-        _check(lib().pt_init(device))
+        ids = list(devices) if devices else [device]
+        arr = (ctypes.c_int32 * len(ids))(*ids)
+        _check(lib().pt_init(len(ids), arr))
         self._s = ctypes.c_void_p()
         _check(lib().pt_scene_create(host.desc, ctypes.byref(self._s)))
         if batch_slots:
@@ -417,3 +433,42 @@ def exported_symbols() -> list:
     text = open(hdr).read()
     decl = re.compile(r"^(?:const\s+)?[a-z_]+\s*\*?\s*(pt_[a-z0-9_]+)\s*\(", re.M)
     return sorted(set(decl.findall(text)))
+
+
+def comm_unique_id() -> bytes:
+    """pt_comm_unique_id: the RCCL unique id rank 0 hands to every rank."""
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().pt_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """pt_comm: RCCL communicator of a multi-process job on the current GPU."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        if len(uid) != 128:
+            raise ValueError("unique id must be 128 bytes")
+        self.nranks, self.rank = nranks, rank
+        self._c = ctypes.c_void_p()
+        _check(lib().pt_comm_create(nranks, rank, uid, ctypes.byref(self._c)))
+
+    def render_frame(self, scene: "Scene", d_accum: int, stream: int = 0) -> dict:
+        """pt_render_frame_dist: tiles t % nranks == rank, then the film reduce to rank 0."""
+        st = pt_stats()
+        _check(lib().pt_render_frame_dist(scene._s, self._c, ctypes.c_void_p(d_accum), ctypes.c_void_p(stream),
+                                          ctypes.byref(st)))
+        return st.as_dict()
+
+    def reduce(self, scene: "Scene", d_accum: int, root: int = 0, stream: int = 0) -> None:
+        _check(lib().pt_film_reduce(self._c, scene._s, ctypes.c_void_p(d_accum), root, ctypes.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self._c:
+            lib().pt_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

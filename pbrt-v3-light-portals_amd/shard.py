@@ -5,14 +5,16 @@ tiles (SamplerIntegrator::Render, src/core/integrator.cpp:526-637;
 ParallelFor2D, src/core/parallel.cpp).  Every (pixel, sample) path is
 independent, so the units shard with no data-path collective:
 
-  * "samples" (default, weak scaling): rank r renders camera-sample indices
-    [r*spp, (r+1)*spp) of every pixel -- the Halton sequence simply continues
-    (HaltonSampler::GetIndexForSample, src/samplers/halton.cpp:96-110), so N
-    ranks together produce the frame at N*spp.
+  * "tiles" (default, strong scaling): rank r renders tiles t with
+    t % N == r at the full spp -- the reference's 16x16 tile loop
+    (integrator.cpp:533-538) dealt round-robin; 1/2/4/8 ranks render the same
+    frame.
   * "samples-split" (strong scaling): the scene's spp are divided among the
     ranks, rank r renders [spp*r//N, spp*(r+1)//N).
-  * "tiles" (strong scaling): rank r renders tiles t with t % N == r at the
-    full spp -- the reference's tile loop dealt round-robin.
+  * "samples" (opt-in WEAK scaling): rank r renders camera-sample indices
+    [r*spp, (r+1)*spp) of every pixel -- the Halton sequence simply continues
+    (HaltonSampler::GetIndexForSample, src/samplers/halton.cpp:96-110), so N
+    ranks together produce a different, N*spp frame.
 
 Each rank accumulates Film::Pixel (XYZ sum + filter-weight sum, film.h:98-105)
 for its units; the films combine by addition (Film::MergeFilmTile is a sum,
@@ -24,7 +26,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Callable, Optional
 
-MODES = ("samples", "samples-split", "tiles")
+MODES = ("tiles", "samples-split", "samples")
 
 
 @dataclass(frozen=True)
@@ -41,7 +43,7 @@ class Shard:
         return self.sample_end - self.sample_begin
 
 
-def plan(rank: int, world: int, spp: int, mode: str = "samples") -> Shard:
+def plan(rank: int, world: int, spp: int, mode: str = "tiles") -> Shard:
     """The units rank `rank` of `world` renders for a scene with `spp` samples
     per pixel."""
     if world < 1 or not 0 <= rank < world:
@@ -82,5 +84,11 @@ def device_renderer(scene, d_accum_ptr: int, stream: int) -> Callable[[Shard], d
 
 
 def reduce_to_root(accum) -> None:
+    """torch.distributed reduce (the gloo CPU tests; the GPU bench reduces
+    with the library's own RCCL communicator, ptgpu.Comm)."""
     import torch.distributed as dist
     dist.reduce(accum, dst=0)
+
+
+def scaling(mode: str) -> str:
+    return "weak" if mode == "samples" else "strong"

@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ptgpu.lib().pt_abi_version() == 4
+    assert ptgpu.lib().pt_abi_version() == 5
 
 
 def test_pt_h_compiles_as_c():
@@ -72,3 +72,35 @@ def test_ctypes_mirror_matches_c_layout():
     import ctypes
     D = ptgpu.pt_scene_desc
     assert got == [ctypes.sizeof(D), D.integrator.offset, D.n_spheres.offset, ctypes.sizeof(ptgpu.pt_material)]
+
+
+def test_bvh_host_capacities(tmp_path):
+    """pt_build_bvh_host reports node and prim counts separately and rejects
+    buffers smaller than them (a single 3-4-primitive leaf has n_nodes = 1 <
+    n_prims)."""
+    import ctypes
+    import numpy as np
+    from conftest import scene_variant
+    hs = ptgpu.HostScene(scene_variant(tmp_path, res=(8, 8), spp=1))
+    nodes, order = hs.bvh()
+    assert sorted(order.tolist()) == list(range(len(order)))
+    L = ptgpu.lib()
+    n, m = ctypes.c_int32(), ctypes.c_int32()
+    small = np.zeros(8 * len(nodes), np.uint32)
+    o = np.zeros(len(order), np.int32)
+    assert L.pt_build_bvh_host(hs.desc, ctypes.byref(n), small.ctypes.data, len(nodes) - 1, ctypes.byref(m),
+                               None, 0) == 1
+    assert L.pt_build_bvh_host(hs.desc, ctypes.byref(n), None, 0, ctypes.byref(m), o.ctypes.data,
+                               len(order) - 1) == 1
+    assert (n.value, m.value) == (len(nodes), len(order))
+
+
+def test_multi_gpu_entry_points_reject_bad_arguments():
+    """pt_init / the RCCL communicator entry points validate before touching
+    a device (no GPU here: the device-less calls fail with a status)."""
+    L = ptgpu.lib()
+    assert L.pt_init(0, None) != 0
+    assert L.pt_comm_create(0, 0, None, None) == 1
+    assert L.pt_film_reduce(None, None, None, 0, None) == 1
+    assert L.pt_render_frame_dist(None, None, None, None, None) == 1
+    assert L.pt_shutdown() == 0
