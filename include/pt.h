@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5
+#define PT_ABI_VERSION 6
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -257,6 +257,13 @@ typedef struct pt_scene_desc {
     int32_t spectral;
     const float* material_s60; /* n_materials x 3 x 60: matte Kd | -, glass / dispersive_glass -, Kr, Kt; mirror -, Kr */
     const float* light_s60;    /* n_lights x 60: area lights' Lemit = L * scale (infinite lights use their RGB L) */
+    /* Optional prebuilt BVH: the reference's flattened BVHAccel::nodes
+     * (32-byte LinearBVHNode records, bvh.cpp:95-104).  When bvh_nodes is
+     * non-NULL, prims[] are in the BVH's primitive order
+     * (BVHAccel::primitives) and pt_scene_create builds no BVH of its own;
+     * NULL / 0: the SAH build of bvh.cpp:236-402 runs on prims[] in scene order. */
+    int32_t n_bvh_nodes;
+    const void* bvh_nodes;
 } pt_scene_desc;
 
 /* ---- statistics (reference counters, src/core/scene.cpp:40-42 etc.) ---- */

@@ -572,6 +572,19 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     if (bvh_src) {
         s->host_nodes = bvh_src->host_nodes;
         s->host_prim_order = bvh_src->host_prim_order;
+    } else if (d->bvh_nodes) {  // the caller's (the reference's) flattened BVH, prims in its order
+        if (d->n_bvh_nodes <= 0) throw PtError(PT_ERR_INVALID_ARG, "prebuilt BVH without nodes");
+        const LinearNode* nn = (const LinearNode*)d->bvh_nodes;
+        s->host_nodes.assign(nn, nn + d->n_bvh_nodes);
+        for (int i = 0; i < d->n_bvh_nodes; ++i) {
+            const LinearNode& n = s->host_nodes[i];
+            const bool ok = n.nprims > 0 ? (n.offset >= 0 && (int64_t)n.offset + n.nprims <= d->n_prims)
+                                         : (n.offset > i && n.offset < d->n_bvh_nodes && i + 1 < d->n_bvh_nodes &&
+                                            n.axis < 3);
+            if (!ok) throw PtError(PT_ERR_INVALID_ARG, "prebuilt BVH node " + std::to_string(i) + " out of range");
+        }
+        s->host_prim_order.resize((size_t)d->n_prims);
+        for (int i = 0; i < d->n_prims; ++i) s->host_prim_order[i] = i;
     } else
         build_bvh(d, &s->host_nodes, &s->host_prim_order);
     std::vector<float4> nodes(2 * s->host_nodes.size());

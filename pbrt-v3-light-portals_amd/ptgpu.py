@@ -174,7 +174,8 @@ class pt_scene_desc(ctypes.Structure):
         ("portals", ctypes.c_void_p), ("bvh_max_prims", ctypes.c_int32), ("camera", pt_camera_desc),
         ("film", pt_film_desc), ("sampler", pt_sampler_desc), ("integrator", pt_integrator_desc),
         ("n_spheres", ctypes.c_int32), ("spheres", ctypes.c_void_p), ("spectral", ctypes.c_int32),
-        ("material_s60", ctypes.POINTER(ctypes.c_float)), ("light_s60", ctypes.POINTER(ctypes.c_float))]
+        ("material_s60", ctypes.POINTER(ctypes.c_float)), ("light_s60", ctypes.POINTER(ctypes.c_float)),
+        ("n_bvh_nodes", ctypes.c_int32), ("bvh_nodes", ctypes.c_void_p)]
 
 
 def scene_desc(hs: "HostScene") -> pt_scene_desc:
