@@ -84,27 +84,43 @@ def scene_text(args) -> str:
     return txt
 
 
+# The reference itself, timed by the survey in this container (SURVEY.md §6 /
+# §8(d) [probe]): built from its sources with logging / EXR shims outside the
+# repo, 8 threads on the draft C2 scene.  Reported beside the port's own rate.
+REFERENCE_PROBE = {"value": 0.684, "unit": "Msamples/s", "cores": 8,
+                   "source": "SURVEY.md §8(d) [probe]: reference pbrt-v3-light-portals, --nthreads 8, "
+                             "draft C2 scene at 480x270 @16 spp scaled to the frame (not re-run here)"}
+
+
 def cpu_baseline(scene_path: str, seconds: float) -> dict:
     """Reference CPU path restated in C (oracle/, 'port'), timed on this host's
-    cores on a bounded sample: the first T 16x16 tiles of the same frame."""
+    cores on a bounded sample of the same frame: the 16x16 tiles t with
+    t % stride == 0, spread over the whole image (stride sized so the timed
+    run takes about `seconds`)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import ptgpu
     hs = ptgpu.HostScene(scene_path)
     threads = max(1, min(16, os.cpu_count() or 1))
+    w, h = hs.film_size()
+    ntiles = ((w + 15) // 16) * ((h + 15) // 16)
+    stride = max(1, ntiles // (2 * threads))
     t0 = time.perf_counter()
-    _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=2 * threads)
+    _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
-    rate = st["samples"] / dt
-    per_tile = st["samples"] / (2 * threads)
-    tiles = int(max(2 * threads, min(4000, rate * seconds / per_tile)))
+    per_tile = st["samples"] / max(1, (ntiles + stride - 1) // stride)
+    want = max(2 * threads, min(ntiles, st["samples"] / dt * seconds / per_tile))
+    stride = max(1, int(ntiles // want))
     t0 = time.perf_counter()
-    _, st = pyoracle.render(hs.desc, nthreads=threads, max_tiles=tiles)
+    _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
-    return {"value": round(st["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"first {tiles} 16x16 tiles of the same frame at the scene's spp "
-                      f"({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
-            "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3)}
+    rate = st["samples"] / dt / 1e6
+    return {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"every {stride}th 16x16 tile of the same frame (tiles t % {stride} == 0 over the whole image) "
+                      f"at the scene's spp ({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
+            "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3),
+            "per_thread": round(rate / threads, 4),
+            "reference_probe": dict(REFERENCE_PROBE, per_thread=round(REFERENCE_PROBE["value"] / 8, 4))}
 
 
 def pmc_traffic(workload: str, kernel: str = "k_trace"):
@@ -127,6 +143,53 @@ def pmc_traffic(workload: str, kernel: str = "k_trace"):
     return None, None
 
 
+def rooflines(agg: dict, workload: str, lds_scene: bool) -> dict:
+    """roofline = the dominant kernel by measured time (HIP events around every
+    launch on its stream); both kernels' figures under roofline_kernels.
+
+    * k_trace: algorithmic bytes per SURVEY §8(d), 32 B per node visit + 48 B
+      per primitive test, counted on the device.  For a scene whose BVH fits
+      LDS (C2) those bytes are LDS reads, not HBM traffic: the kernel is then
+      labelled on-chip / latency-bound and only its PMC-measured HBM bytes
+      (rays in, hits out) are set against the HBM peak.
+    * k_shade: the path-state bytes each path step must read and write (the
+      SoA fields PathIntegrator::Li carries between vertices + queue
+      entries), counted on the device per step (kernels.hip shade_path)."""
+    ks = {}
+    tl, sl = max(1, agg["trace_launches"]), max(1, agg["shade_launches"])
+    alg_t = (32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]) / tl
+    avg_t = agg["trace_ms"] / tl
+    trf_t, src_t = pmc_traffic(workload, "k_trace")
+    ks["k_trace"] = {"avg_launch_ms": round(avg_t, 4), "algorithmic_bytes_per_launch": round(alg_t, 1),
+                     "algorithmic_GBs": round(alg_t / (avg_t * 1e-3) / 1e9, 1) if avg_t > 0 else 0.0,
+                     "data": "LDS (BVH + primitives staged per block): on-chip, latency-bound" if lds_scene else "HBM",
+                     "hbm_traffic_per_launch": round(trf_t, 1) if trf_t is not None else None,
+                     "hbm_GBs": round(trf_t / (avg_t * 1e-3) / 1e9, 1) if (trf_t is not None and avg_t > 0) else None,
+                     "traffic_source": src_t, "total_ms": round(agg["trace_ms"], 2)}
+    if agg["shade_bytes"] > 0:
+        alg_s = agg["shade_bytes"] / sl
+        avg_s = agg["shade_ms"] / sl
+        trf_s, src_s = pmc_traffic(workload, "k_shade")
+        ks["k_shade"] = {"avg_launch_ms": round(avg_s, 4), "algorithmic_bytes_per_launch": round(alg_s, 1),
+                         "algorithmic_GBs": round(alg_s / (avg_s * 1e-3) / 1e9, 1) if avg_s > 0 else 0.0,
+                         "data": "HBM (SoA path state)",
+                         "hbm_traffic_per_launch": round(trf_s, 1) if trf_s is not None else None,
+                         "hbm_GBs": round(trf_s / (avg_s * 1e-3) / 1e9, 1) if (trf_s is not None and avg_s > 0) else None,
+                         "traffic_source": src_s, "total_ms": round(agg["shade_ms"], 2)}
+    dom = max(ks, key=lambda k: ks[k]["total_ms"])
+    k = ks[dom]
+    on_chip = dom == "k_trace" and lds_scene
+    achieved = k["hbm_GBs"] if on_chip else k["algorithmic_GBs"]
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved is not None else None,
+            "traffic": k["hbm_traffic_per_launch"], "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + "
+            "WRITE_SIZE passes)", "traffic_source": k["traffic_source"], "kernel": dom,
+            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"]}
+    if on_chip:
+        roof["note"] = "dominant kernel reads its scene from LDS: achieved = measured HBM bytes / launch time"
+    return {"roofline": roof, "roofline_kernels": ks}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +210,8 @@ def main():
     hs = ptgpu.HostScene(spath)
     sc = ptgpu.Scene(hs, device=local, batch_slots=args.batch_slots or None)
     w, h = sc.film_size()
+    nodes, order = hs.bvh()
+    lds_scene = (32 * len(nodes) + 48 * len(order)) <= 16384  # render.hip: k_trace stages such a BVH in LDS
     import re
     spp = int(re.search(r'"integer pixelsamples" \[(\d+)\]', open(spath).read()).group(1))
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -173,7 +238,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     agg = {"samples": 0, "closest_rays": 0, "shadow_rays": 0, "node_visits": 0, "prim_tests": 0, "trace_ms": 0.0,
-           "trace_launches": 0}
+           "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0}
     for _ in range(args.steps):
         st = step()
         for k in agg:
@@ -198,9 +263,6 @@ def main():
         cname, cdepth, cdata = CONFIGS[args.config][1:]
         workload = (f"{cname} {w}x{h} @{spp}spp{'/rank' if args.shard == 'samples' else ''}, "
                     f"{cdepth}, {args.shard}-sharded")
-        traffic, traffic_src = pmc_traffic(workload)
-        alg_bytes = 32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]
-        achieved = alg_bytes / (agg["trace_ms"] * 1e-3) / 1e9 if agg["trace_ms"] > 0 else 0.0
         out = {
             "metric": METRIC,
             "value": round(total_samples / dt / 1e6, 3),
@@ -219,14 +281,8 @@ def main():
                        "parallelism": f"{args.shard} x{world}"},
             "mrays_per_s": round(total_rays / dt / 1e6, 2),
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": round(traffic, 1) if traffic is not None else None,
-                         "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
-                         "kernel": "k_trace", "algorithmic_bytes_per_launch": round(
-                             alg_bytes / max(1, agg["trace_launches"]), 1),
-                         "avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4)},
         }
+        out.update(rooflines(agg, workload, lds_scene))
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spath, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 6
+#define PT_ABI_VERSION 7
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -275,8 +275,11 @@ typedef struct pt_stats {
     uint64_t prim_tests;       /* leaf primitive intersection tests */
     uint64_t samples;          /* camera samples rendered */
     double render_ms;          /* device wall time of the render (events) */
-    double trace_ms;           /* summed duration of the trace kernel */
+    double trace_ms;           /* summed duration of the trace kernel (HIP events on the launch stream) */
     uint64_t trace_launches;
+    double shade_ms;           /* summed duration of the shading kernel */
+    uint64_t shade_launches;
+    uint64_t shade_bytes;      /* path integrator: algorithmic path-state bytes the shading kernel moved */
 } pt_stats;
 
 /* ---- host scene loader (.pbrt subset) ---- */

@@ -215,7 +215,7 @@ struct DevStats {
     unsigned long long dim_overflow;
     unsigned long long lane_iters;  // k_trace_pt: lane-iterations executed (SIMD slots)
     unsigned long long lane_steps;  // k_trace_pt: node visits + primitive tests performed
-    unsigned long long pad;
+    unsigned long long shade_bytes;  // k_shade (path integrator): algorithmic path-state bytes moved
 };
 
 }  // namespace pt

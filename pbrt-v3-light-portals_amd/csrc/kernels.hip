@@ -775,7 +775,8 @@ __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int 
 // selected portal is call-local.  Returns true when ray A was emitted.
 template <int kFt>
 __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
-                                           const SurfHit& it, const Bsdf& bsdf, float u10, float u11) {
+                                           const SurfHit& it, const Bsdf& bsdf, float u10, float u11,
+                                           uint32_t* ab = nullptr) {
     const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
     const DevPlane& lp = sc.planes[PT_IDX(l.shape, sc.n_planes)];
     const uint32_t N = (uint32_t)ps.n;
@@ -846,6 +847,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                     }
                     flags |= kNfDivPortal;
                     put_nee(ps, slot, kNeePortalPdf, portalPdf);
+                    if (ab) *ab += 4;
                 }
                 if (pdf > 0) {
                     const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
@@ -854,8 +856,10 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                     put_nee(ps, slot, kNeePdf, pdf);
                     put_nee3(ps, slot, kNeeLi, s3(0.f));
                     flags |= kNfA;
+                    if (ab) *ab += 24 + 12 + 4 + 12;
                 }
                 put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+                if (ab) *ab += 4;
                 return (flags & kNfA) != 0;
             }
         }
@@ -871,8 +875,10 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
         put_nee(ps, slot, kNeePdf, pdf);
         put_nee3(ps, slot, kNeeLi, Li);
         flags |= kNfA;
+        if (ab) *ab += 24 + 12 + 4 + 12;
     }
     put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+    if (ab) *ab += 4;
     return (flags & kNfA) != 0;
 }
 
@@ -881,7 +887,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
 template <int kFt>
 __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                             const SurfHit& it, const Bsdf& bsdf, float ul0, float ul1, float us0,
-                                            float us1) {
+                                            float us1, uint32_t* ab = nullptr) {
     const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
     const uint32_t N = (uint32_t)ps.n;
     uint32_t flags = kNfMis;
@@ -907,6 +913,7 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
                 put_nee3(ps, slot, kNeeF, ((f * Li) * lightWeight) / lightPdf);
             }
             flags |= kNfA | kNfC1;
+            if (ab) *ab += 28 + 12;
         }
     }
     if (l.kind != PT_LIGHT_POINT) {  // BSDF sampling only for non-delta lights
@@ -926,24 +933,42 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
                 put_nee(ps, slot, kNeeSpdf, pdf2);
                 put_nee(ps, slot, kNeeLight, __int_as_float(lightIdx));
                 flags |= kNfB;
+                if (ab) *ab += 24 + 12 + 4 + 4 + 4;
             }
         }
     }
     put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
+    if (ab) *ab += 4;
     return flags;
 }
 
 // One path step.  Returns the rays to enqueue in rays[] and whether the path
 // stays alive.
 template <int kFt>
+// ab: algorithmic path-state bytes this step reads and writes (the bench's
+// k_shade roofline): the SoA fields the reference's Li loop carries from one
+// vertex to the next, plus the queue entries (scene tables are not counted).
 __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
-                                           uint32_t* nrays, bool* keep, bool* overflow) {
+                                           uint32_t* nrays, bool* keep, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     *nrays = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
     uint32_t st = ps.st[slot];
     S3 L = load_s3(ps.L, N, slot);
+    *ab += 4 + 4 + 12 + 12 + 4;  // queue entry, st + L read, L + st written
     if (st & kStNee) {
+        {   // bytes of the NEE payload resolve_nee reads (integrator.cpp:121, portal_arealight.cpp:29-239)
+            const uint32_t fl = __float_as_uint(ps.nee[kNeeFlags * N + slot]);
+            uint32_t b = 4 + 12 + 4;  // flags, beta, light-selection pdf
+            if (fl & kNfPortal) {
+                if (fl & kNfA) b += 12 + 4 + 12 + 4 + (ps.hitA[slot] >= 0 ? 24 : 0);
+                if (fl & kNfDivPortal) b += 4;
+            } else if (fl & kNfMis) {
+                if (fl & kNfC1) b += 4 + 12;
+                if (fl & kNfB) b += 4 + 4 + 12 + 4 + 4 + (ps.hitB[slot] >= 0 ? 24 : 0);
+            }
+            *ab += b;
+        }
         resolve_nee<kFt>(sc, ps, slot, &L);
         st &= ~kStNee;
     }
@@ -954,6 +979,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         const Ray ray = load_ray6(ps.ray, N, slot, kInf);
         const int hp = ps.hit[slot];
         S3 beta = load_s3(ps.beta, N, slot);
+        *ab += 24 + 4 + 12;
         SurfHit si;
         bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &si);
         int mat = -1, light = -1;
@@ -969,10 +995,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
                 const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
                 store_ray6(ps.ray, N, slot, r);
+                *ab += 24;
                 st |= kStCont;
                 rays[(*nrays)++] = slot << 2 | kRayCont;
             } else {
                 Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+                *ab += 4;
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
                 const float wvl0 = Ft<kFt>::spec && sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_DISPERSIVE_GLASS
@@ -992,12 +1020,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                             const float uL0 = dm.get1(), uL1 = dm.get1();
                             const float uS0 = dm.get1(), uS1 = dm.get1();
                             if (sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
-                                if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1)) {
+                                if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1, ab)) {
                                     rays[(*nrays)++] = slot << 2 | kRayA;
                                     deferred = true;
                                 }
                             } else {
-                                const uint32_t f = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1);
+                                const uint32_t f = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1, ab);
                                 if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
                                 if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
                                 deferred = (f & (kNfA | kNfB)) != 0;
@@ -1007,6 +1035,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                     if (deferred) {
                         put_nee3(ps, slot, kNeeBeta, beta);
                         put_nee(ps, slot, kNeeLpdf, lightPdf);
+                        *ab += 12 + 4;
                         st |= kStNee;
                     } else {
                         // no ray: EstimateDirect returned Spectrum(0)
@@ -1026,7 +1055,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                     if (Ft<kFt>::spec && (sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
                         const float eta = bsdf.eta;
                         ps.eta[slot] *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                        *ab += 4;
                     }
+                    *ab += 4;  // etaScale read for Russian roulette
                     const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     bool alive = true;
                     // Russian roulette (path.cpp:177-185)
@@ -1039,6 +1070,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                     if (alive) {
                         store_ray6(ps.ray, N, slot, r);
                         store_s3(ps.beta, N, slot, beta);
+                        *ab += 24 + 12;
                         ++bounces;
                         st |= kStCont;
                         rays[(*nrays)++] = slot << 2 | kRayCont;
@@ -1053,6 +1085,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
     store_s3(ps.L, N, slot, L);
     ps.st[slot] = st;
     *keep = (st & (kStCont | kStNee)) != 0;
+    *ab += 4 * (*nrays + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
 
 template <int kFt>
@@ -1063,6 +1096,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     const uint32_t n = *pq_count;
     bool overflow = false;
     PT_WAVEQ(wq);
+    uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         uint32_t rays[3];
@@ -1071,12 +1105,14 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         uint32_t slot = 0;
         if (i < n) {
             slot = pq[i];
-            shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
+            shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow, &ab);
         }
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
+    const unsigned long long abw = wave_sum_u64((unsigned long long)ab);
+    if (lane_id() == 0 && abw) atomicAdd(&stats->shade_bytes, abw);
 }
 
 // ----------------------------------------------------------------------------

@@ -970,8 +970,8 @@ __global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
 
 struct RenderResult {
     DevStats st{};
-    double render_ms = 0, trace_ms = 0;
-    uint64_t launches = 0, samples = 0;
+    double render_ms = 0, trace_ms = 0, shade_ms = 0;
+    uint64_t launches = 0, samples = 0, shade_launches = 0;
 };
 
 // Render the given tiles into the device accumulation buffer d_accum
@@ -1070,8 +1070,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         }
         return tev[i];
     };
-    double trace_ms = 0;
+    double trace_ms = 0, shade_ms = 0;
     size_t tcount = 0;
+    std::vector<size_t> shade_ev;  // tev indices of the shading launches
     // PT_SYNC_CHECK=1 (diagnostics): synchronise after every launch so a
     // device fault is reported against the kernel and bounce that raised it.
     const bool syncCheck = std::getenv("PT_SYNC_CHECK") != nullptr;
@@ -1132,6 +1133,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     sync_check("k_trace", iter);
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
+                const size_t sev = tcount++;
+                shade_ev.push_back(sev);
+                HIPCHK(hipEventRecord(tev_get(sev).first, stream));
                 if (s->hero) {
                     hipLaunchKernelGGL(s->hero_waves == 1 ? k_shade_hero : (s->hero_waves == 2 ? k_shade_hero_w2 : k_shade_hero_w4), sg, dim3(kShadeBlock), 0, stream, s->dev, s->hh, ps, hps, pq_in,
                                        counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
@@ -1142,6 +1146,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                                        rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }
                 HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(tev_get(sev).second, stream));
                 sync_check("k_shade", iter);
                 HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
@@ -1173,12 +1178,16 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
     rr.render_ms = ms;
+    std::vector<char> is_shade(tcount, 0);
+    for (size_t i : shade_ev) is_shade[i] = 1;
     for (size_t i = 0; i < tcount; ++i) {
         float t = 0;
         HIPCHK(hipEventElapsedTime(&t, tev[i].first, tev[i].second));
-        trace_ms += t;
+        (is_shade[i] ? shade_ms : trace_ms) += t;
     }
     rr.trace_ms = trace_ms;
+    rr.shade_ms = shade_ms;
+    rr.shade_launches = shade_ev.size();
     for (auto& e : tev) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -1253,6 +1262,9 @@ static void fill_stats(const RenderResult& r, pt_stats* st) {
     st->render_ms = r.render_ms;
     st->trace_ms = r.trace_ms;
     st->trace_launches = r.launches;
+    st->shade_ms = r.shade_ms;
+    st->shade_launches = r.shade_launches;
+    st->shade_bytes = r.st.shade_bytes;
 }
 
 template <class F>
@@ -1354,6 +1366,9 @@ static void add_stats(RenderResult* a, const RenderResult& b) {
     a->samples += b.samples;
     a->launches += b.launches;
     a->trace_ms += b.trace_ms;
+    a->shade_ms += b.shade_ms;
+    a->shade_launches += b.shade_launches;
+    a->st.shade_bytes += b.st.shade_bytes;
     a->render_ms = std::max(a->render_ms, b.render_ms);
 }
 

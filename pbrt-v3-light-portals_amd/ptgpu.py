@@ -37,7 +37,8 @@ class pt_stats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
                 ("prim_tests", ctypes.c_uint64), ("samples", ctypes.c_uint64),
                 ("render_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-                ("trace_launches", ctypes.c_uint64)]
+                ("trace_launches", ctypes.c_uint64), ("shade_ms", ctypes.c_double),
+                ("shade_launches", ctypes.c_uint64), ("shade_bytes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
