@@ -4,10 +4,23 @@
 // 12-bucket SAH, same leaf rule, and the same libstdc++ std::partition /
 // std::nth_element on the primitives in scene order.  The device traverses
 // the resulting 32-byte nodes.
+//
+// Parallel build, same tree: the two children of a node partition disjoint
+// ranges [start, mid) and [mid, end) of the primitive-info array, so the top
+// subtrees run on their own threads without changing any partition.  The
+// reference appends a leaf's primitives to orderedPrims in creation order
+// (depth first, left child first), which visits the leaf ranges in increasing
+// order -- so orderedPrims is simply the final info array, and a leaf's
+// firstPrimOffset is its range start.  Node creation order does not matter:
+// flattenBVHTree numbers the nodes depth first.
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cstring>
+#include <deque>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "host_common.h"
 
@@ -54,29 +67,31 @@ struct BuildNode {
     int splitAxis, firstPrimOffset, nPrimitives;
 };
 
+constexpr int kParallelMin = 1 << 15;  // subtrees smaller than this stay on their thread
+
 struct Builder {
     int maxPrimsInNode;
     std::vector<PrimInfo>& info;
-    std::vector<int>& ordered;
-    std::vector<std::unique_ptr<BuildNode>> pool;
-    int totalNodes = 0;
+    std::atomic<int> totalNodes{0};
+    std::mutex mu;
+    std::vector<std::unique_ptr<std::deque<BuildNode>>> pools;  // one per build thread
 
-    BuildNode* alloc() {
-        pool.emplace_back(new BuildNode());
-        ++totalNodes;
-        return pool.back().get();
+    std::deque<BuildNode>* new_pool() {
+        std::lock_guard<std::mutex> lk(mu);
+        pools.emplace_back(new std::deque<BuildNode>());
+        return pools.back().get();
     }
     void leaf(BuildNode* node, int start, int end, const BBox& bounds) {
-        int first = (int)ordered.size();
-        for (int i = start; i < end; ++i) ordered.push_back((int)info[i].primitiveNumber);
-        node->firstPrimOffset = first;
+        node->firstPrimOffset = start;  // orderedPrims == info after the build (see above)
         node->nPrimitives = end - start;
         node->bounds = bounds;
         node->children[0] = node->children[1] = nullptr;
     }
 
-    BuildNode* build(int start, int end) {
-        BuildNode* node = alloc();
+    BuildNode* build(int start, int end, std::deque<BuildNode>* pool, int par) {
+        pool->emplace_back();
+        BuildNode* node = &pool->back();
+        ++totalNodes;
         BBox bounds = bb_empty();
         for (int i = start; i < end; ++i) bounds = bb_union(bounds, info[i].bounds);
         int nPrimitives = end - start;
@@ -133,8 +148,16 @@ struct Builder {
                 return node;
             }
         }
-        BuildNode* c0 = build(start, mid);
-        BuildNode* c1 = build(mid, end);
+        BuildNode *c0 = nullptr, *c1 = nullptr;
+        if (par > 0 && nPrimitives >= kParallelMin) {  // left subtree on its own thread
+            std::deque<BuildNode>* lp = new_pool();
+            std::thread t([&] { c0 = build(start, mid, lp, par - 1); });
+            c1 = build(mid, end, pool, par - 1);
+            t.join();
+        } else {
+            c0 = build(start, mid, pool, 0);
+            c1 = build(mid, end, pool, 0);
+        }
         node->children[0] = c0;
         node->children[1] = c1;
         node->bounds = bb_union(c0->bounds, c1->bounds);
@@ -204,17 +227,29 @@ void build_bvh(const pt_scene_desc* d, std::vector<LinearNode>* nodes, std::vect
     nodes->clear();
     prim_order->clear();
     if (d->n_prims <= 0) return;
+    const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<PrimInfo> info((size_t)d->n_prims);
-    for (int i = 0; i < d->n_prims; ++i) {
-        info[i].primitiveNumber = (size_t)i;
-        info[i].bounds = prim_world_bound(d, i);
-        info[i].centroid = .5f * info[i].bounds.pmin + .5f * info[i].bounds.pmax;
+    {   // primitive bounds (BVHPrimitiveInfo, bvh.cpp:206-209), in parallel slices
+        std::vector<std::thread> th;
+        const int n = d->n_prims, per = (n + hw - 1) / hw;
+        for (int t = 0; t < hw; ++t)
+            th.emplace_back([&, t] {
+                for (int i = t * per; i < std::min(n, (t + 1) * per); ++i) {
+                    info[i].primitiveNumber = (size_t)i;
+                    info[i].bounds = prim_world_bound(d, i);
+                    info[i].centroid = .5f * info[i].bounds.pmin + .5f * info[i].bounds.pmax;
+                }
+            });
+        for (auto& t : th) t.join();
     }
     int maxPrims = d->bvh_max_prims > 0 ? std::min(255, d->bvh_max_prims) : 4;
-    Builder b{maxPrims, info, *prim_order, {}, 0};
-    prim_order->reserve((size_t)d->n_prims);
-    BuildNode* root = b.build(0, d->n_prims);
-    nodes->resize((size_t)b.totalNodes);
+    Builder b{maxPrims, info};
+    int par = 0;
+    while ((1 << par) < hw) ++par;
+    BuildNode* root = b.build(0, d->n_prims, b.new_pool(), par);
+    prim_order->resize((size_t)d->n_prims);
+    for (int i = 0; i < d->n_prims; ++i) (*prim_order)[i] = (int)info[i].primitiveNumber;
+    nodes->resize((size_t)b.totalNodes.load());
     int off = 0;
     flatten(root, *nodes, &off);
 }

@@ -543,6 +543,24 @@ def test_killeroo_atrium_matches_oracle(tmp_path):
         assert gst[k] == rst[k], k
 
 
+def test_killeroo_atrium_full_scale_matches_oracle(tmp_path):
+    """Config 5 as benchmarked: scenes/killeroo_atrium.pbrt, 300 Loop-
+    subdivided killeroos, 9.98 M triangles, 17.95 M BVH nodes (prim indices far
+    above 2^23, a stack deeper than the LDS rows: k_trace_pt's spill path), at
+    a 64x36 @2 film: device == oracle bit for bit with identical traversal
+    counters."""
+    from conftest import scene_variant
+    hs, sc = _scene(scene_variant(tmp_path, name="killeroo_atrium.pbrt", res=(64, 36), spp=2))
+    assert hs.film_size() == (64, 36)
+    ref, rst = pyoracle.render(hs.desc, nthreads=16)
+    got, gst = sc.render()
+    print(f"atrium300: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g} nodes={gst['node_visits']}")
+    assert ref.mean() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
+
+
 LAMP_AS_PATH = [('Integrator "directlighting"', 'Integrator "path" "integer maxdepth" [5]'),
                 ('"integer maxdepth" [100]', '')]
 

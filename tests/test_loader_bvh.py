@@ -93,7 +93,8 @@ WorldEnd
 
 
 @pytest.mark.parametrize("n,seed,maxprims", [(1, 0, 4), (2, 1, 4), (3, 2, 4), (17, 3, 4), (500, 4, 4),
-                                             (2000, 5, 1), (2000, 6, 8)])
+                                             (2000, 5, 1), (2000, 6, 8),
+                                             (150000, 7, 4)])  # > 2 x 32K: the threaded subtree build
 def test_bvh_random_soups(tmp_path, n, seed, maxprims):
     hs = ptgpu.HostScene(_soup_scene(tmp_path, n, seed, maxprims=maxprims))
     n1, o1 = hs.bvh()
