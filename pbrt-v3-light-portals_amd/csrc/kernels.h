@@ -6,8 +6,19 @@
 
 namespace pt {
 
-constexpr int kTraceBlock = 128;
-constexpr uint32_t kTraceChunk = 512;  // ray-queue entries a k_trace_nb wave takes per atomic  // 2 waves; LDS stack = kStackLds * 128 * 4 B
+constexpr int kTraceBlock = 128;       // 2 waves; LDS stack = kStackLds * 128 * 4 B
+constexpr uint32_t kTraceChunk = 512;  // ray-queue entries a k_trace_nb wave takes per atomic
+// k_trace_nb: node visits / primitive tests per loop iteration for lanes that
+// stay in node / leaf mode (the loop's refill and step-kind bookkeeping is paid
+// once per iteration); C2: 1/1 -> 6/2 took the kernel from 14.2 to 9.2 ms
+#ifndef PT_NODE_STEPS
+#define PT_NODE_STEPS 6
+#endif
+#ifndef PT_LEAF_STEPS
+#define PT_LEAF_STEPS 2
+#endif
+constexpr int kNodeSteps = PT_NODE_STEPS;
+constexpr int kLeafSteps = PT_LEAF_STEPS;
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
 constexpr int kMaxPortals = 64;

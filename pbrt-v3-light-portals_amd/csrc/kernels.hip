@@ -550,7 +550,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
         ++iters;
         bool done = false;
         if (leafStep) {
-            if (wantLeaf) {
+#pragma unroll
+            for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
+                if (!(active && !done && leafPos < leafEnd)) continue;
                 const int pi = leafPos++;
                 ++prims;
                 const float4 r0 = bprims[3 * pi];
@@ -576,27 +578,33 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
                 toVisit -= pop ? 1 : 0;
             }
         } else if (active && !wantLeaf) {
-            const int c = cur;
-            const float4 a = bnodes[2 * c];
-            const float4 b = bnodes[2 * c + 1];
-            ++nodes;
-            const bool hit = node_box_hit(a, b, ray, inv, n0, n1, n2);
-            const int off = __float_as_int(b.z);
-            const uint32_t npax = __float_as_uint(b.w);
-            const int np = (int)(npax & 0xffffu);
-            const int axis = (int)(npax >> 16);
-            const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
-            const bool inner = hit && np == 0;
-            const bool leaf = hit && np > 0;
-            const bool miss = !hit;
-            stk[toVisit * kTraceBlock] = neg ? c + 1 : off;  // push slot (kept only for an inner node)
-            const int popv = stk[max(toVisit - 1, 0) * kTraceBlock];
-            const bool pop = miss && toVisit > 0;
-            done = miss && toVisit == 0;
-            cur = inner ? (neg ? off : c + 1) : (pop ? popv : c);
-            toVisit += inner ? 1 : (pop ? -1 : 0);
-            leafPos = leaf ? off : leafPos;
-            leafEnd = leaf ? off + np : leafEnd;
+            // kNodeSteps node visits per loop iteration for lanes that stay in
+            // node mode (the loop's refill / step-kind bookkeeping is paid once)
+#pragma unroll
+            for (int u = 0; u < kNodeSteps; ++u) {
+                if (u > 0 && (done || leafPos < leafEnd)) continue;
+                const int c = cur;
+                const float4 a = bnodes[2 * c];
+                const float4 b = bnodes[2 * c + 1];
+                ++nodes;
+                const bool hit = node_box_hit(a, b, ray, inv, n0, n1, n2);
+                const int off = __float_as_int(b.z);
+                const uint32_t npax = __float_as_uint(b.w);
+                const int np = (int)(npax & 0xffffu);
+                const int axis = (int)(npax >> 16);
+                const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                const bool inner = hit && np == 0;
+                const bool leaf = hit && np > 0;
+                const bool miss = !hit;
+                stk[toVisit * kTraceBlock] = neg ? c + 1 : off;  // push slot (kept only for an inner node)
+                const int popv = stk[max(toVisit - 1, 0) * kTraceBlock];
+                const bool pop = miss && toVisit > 0;
+                done = miss && toVisit == 0;
+                cur = inner ? (neg ? off : c + 1) : (pop ? popv : c);
+                toVisit += inner ? 1 : (pop ? -1 : 0);
+                leafPos = leaf ? off : leafPos;
+                leafEnd = leaf ? off + np : leafEnd;
+            }
         }
         if (done) {
             if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;

@@ -239,7 +239,7 @@ struct pt_scene {
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
-    int leaf_min = 24;           // lanes parked at leaves that trigger a primitive-test step
+    int leaf_min = 40;           // lanes parked at leaves that trigger a primitive-test step
     int trace_spill = 1;         // BVH deeper than the LDS stack: keep the global spill path
     int stack_rows = pt::kStackLds;  // LDS stack entries per lane in k_trace_pt
     // pt_init(n > 1, ids): one replica per further device of the process
