@@ -328,7 +328,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
     const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
     unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
-    bool active = false, exhausted = false;
+    bool active = false, exhausted = false, drained = false;
+    uint32_t qn = 0, qe = 0;  // the wave's private chunk of the ray queue (as k_trace_nb)
     uint32_t slot = 0, kind = 0;
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
     V3 inv = v3(0, 0, 0);
@@ -340,13 +341,21 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if (nidle > 0 && (nidle >= (uint32_t)refill_min || nidle == 64u)) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(fetch, nidle);
-                base = (uint32_t)__shfl((int)base, 0);
-                if (base + nidle >= n) exhausted = true;
+                if (qn >= qe && !drained) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
+                    base = (uint32_t)__shfl((int)base, 0);
+                    qn = base < n ? base : n;
+                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
+                    drained = base + kTraceChunk >= n;
+                }
+                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
+                const uint32_t k = (uint32_t)__popcll(idle & lower);
+                const uint32_t i = qn + k;
+                qn += take;
+                if (drained && qn >= qe) exhausted = true;
                 if (!active) {
-                    const uint32_t i = base + (uint32_t)__popcll(idle & lower);
-                    if (i < n) {
+                    if (k < take) {
                         const uint32_t e = rq[i];
                         slot = e >> 2;
                         kind = e & 3u;
@@ -386,57 +395,65 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
         if (!active || wantLeaf != leafStep) continue;
         bool done = false;
         if (leafStep) {
-            const int pi = leafPos++;
-            ++prims;
-            const float4 r0 = bprims[3 * pi];
-            const float4 r1 = bprims[3 * pi + 1];
-            const uint32_t fl = __float_as_uint(r0.w);
-            float t;
-            bool ok;
-            if (fl & kPrimAnalytic) {
-                ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
-            } else {
-                const float4 r2 = bprims[3 * pi + 2];
-                ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
-                if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
-            }
-            if (ok) {
-                hitPrim = pi;
-                if (kind == kRayShadow) done = true;
-                else ray.tmax = t;
-            }
-            if (!done && leafPos == leafEnd) {
-                if (toVisit == 0) done = true;
-                else {
-                    --toVisit;
-                    cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
+#pragma unroll
+            for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
+                if (u > 0 && (done || leafPos >= leafEnd)) continue;
+                const int pi = leafPos++;
+                ++prims;
+                const float4 r0 = bprims[3 * pi];
+                const float4 r1 = bprims[3 * pi + 1];
+                const uint32_t fl = __float_as_uint(r0.w);
+                float t;
+                bool ok;
+                if (fl & kPrimAnalytic) {
+                    ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
+                } else {
+                    const float4 r2 = bprims[3 * pi + 2];
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
+                    if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
+                }
+                if (ok) {
+                    hitPrim = pi;
+                    if (kind == kRayShadow) done = true;
+                    else ray.tmax = t;
+                }
+                if (!done && leafPos == leafEnd) {
+                    if (toVisit == 0) done = true;
+                    else {
+                        --toVisit;
+                        cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
+                    }
                 }
             }
         } else {
-            const float4 a = bnodes[2 * cur];
-            const float4 b = bnodes[2 * cur + 1];
-            ++nodes;
-            if (node_box_hit(a, b, ray, inv, n0, n1, n2)) {
-                const int off = __float_as_int(b.z);
-                const uint32_t npax = __float_as_uint(b.w);
-                const int np = (int)(npax & 0xffffu);
-                if (np > 0) {
-                    leafPos = off;
-                    leafEnd = off + np;
+#pragma unroll
+            for (int u = 0; u < kNodeSteps; ++u) {  // up to kNodeSteps node visits while in node mode
+                if (u > 0 && (done || leafPos < leafEnd)) continue;
+                const float4 a = bnodes[2 * cur];
+                const float4 b = bnodes[2 * cur + 1];
+                ++nodes;
+                if (node_box_hit(a, b, ray, inv, n0, n1, n2)) {
+                    const int off = __float_as_int(b.z);
+                    const uint32_t npax = __float_as_uint(b.w);
+                    const int np = (int)(npax & 0xffffu);
+                    if (np > 0) {
+                        leafPos = off;
+                        leafEnd = off + np;
+                    } else {
+                        const int axis = (int)(npax >> 16);
+                        const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
+                        const int far = neg ? cur + 1 : off;
+                        cur = neg ? off : cur + 1;
+                        if (!kSpill || toVisit < stack_rows) stk[toVisit * kTraceBlock + tid] = far;
+                        else myspill[toVisit - stack_rows] = far;
+                        ++toVisit;
+                    }
+                } else if (toVisit == 0) {
+                    done = true;
                 } else {
-                    const int axis = (int)(npax >> 16);
-                    const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
-                    const int far = neg ? cur + 1 : off;
-                    cur = neg ? off : cur + 1;
-                    if (!kSpill || toVisit < stack_rows) stk[toVisit * kTraceBlock + tid] = far;
-                    else myspill[toVisit - stack_rows] = far;
-                    ++toVisit;
+                    --toVisit;
+                    cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
                 }
-            } else if (toVisit == 0) {
-                done = true;
-            } else {
-                --toVisit;
-                cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
             }
         }
         if (done) {

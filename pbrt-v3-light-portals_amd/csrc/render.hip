@@ -239,7 +239,8 @@ struct pt_scene {
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
-    int leaf_min = 40;           // lanes parked at leaves that trigger a primitive-test step
+    int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
+    int leaf_min_pt = 16;        // k_trace_pt (HBM-resident BVHs): the same threshold
     int trace_spill = 1;         // BVH deeper than the LDS stack: keep the global spill path
     int stack_rows = pt::kStackLds;  // LDS stack entries per lane in k_trace_pt
     // pt_init(n > 1, ids): one replica per further device of the process
@@ -1120,7 +1121,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                         auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
                         const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
                         hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0,
-                                           counts + 4, s->refill_min, s->leaf_min, s->stack_rows, w.spill.p,
+                                           counts + 4, s->refill_min, s->leaf_min_pt, s->stack_rows, w.spill.p,
                                            w.stats.p);
                     } else if (s->lds_scene_bytes)
                         hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
@@ -1350,6 +1351,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("PT_LEAF_MIN_PT")) s->leaf_min_pt = std::max(1, std::atoi(t));
     return s;
 }
 
