@@ -25,10 +25,10 @@ __device__ __forceinline__ float radical_inverse_base3(uint32_t a) {  // lowdisc
     return smin((float)rev * invBaseN, kOneMinusEps);
 }
 
-__device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, int dim, uint32_t a) {  // :405-424
-    const DivMagic dm = sc.divs[dim];
-    const uint16_t* perm = sc.perm + sc.prime_sums[dim];
-    uint64_t rev = 0;
+template <typename Rev>
+__device__ __forceinline__ float scrambled_ri_digits(const DevScene& sc, int dim, uint32_t a, const DivMagic& dm,
+                                                     const uint16_t* perm) {
+    Rev rev = 0;
     float invBaseN = 1;
     // Digits four at a time: the digit chain is ALU only, so the four
     // permutation gathers are issued back to back and waited on once (a
@@ -49,12 +49,21 @@ __device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, i
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if ((uint32_t)k < live) {
-                rev = rev * dm.base + pv[k];
+                rev = rev * (Rev)dm.base + (Rev)pv[k];
                 invBaseN *= dm.inv_base;
             }
         }
     }
     return smin(invBaseN * ((float)rev + sc.perm_c0[dim]), kOneMinusEps);
+}
+
+__device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, int dim, uint32_t a) {  // :405-424
+    const DivMagic dm = sc.divs[dim];
+    const uint16_t* perm = sc.perm + sc.prime_sums[dim];
+    // reversedDigits < base^nDigits <= base * a: with base * a < 2^32 the
+    // reference's 64-bit accumulator never leaves 32 bits (same value, same float)
+    if ((uint64_t)a * dm.base < (1ull << 32)) return scrambled_ri_digits<uint32_t>(sc, dim, a, dm, perm);
+    return scrambled_ri_digits<uint64_t>(sc, dim, a, dm, perm);
 }
 
 // dim must be < sc.max_dim (checked by the caller).
@@ -239,9 +248,9 @@ __device__ __forceinline__ V3 vload3(const float* a, int i) { return v3(a[3 * i]
 // (triangle.cpp:297-420, interaction.cpp:44-89).  Returns false when the
 // reference would reject (it never does for the primitive that won in the
 // traversal, which already applied the same tests).
-__device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si) {
+__device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si, V3 p0, V3 p1,
+                                            V3 p2) {
     const pt_triangle tr = sc.tris[PT_IDX(ti, sc.n_tris)];
-    V3 p0 = vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)), p1 = vload3(sc.P, PT_IDX(tr.v[1], sc.n_verts)), p2 = vload3(sc.P, PT_IDX(tr.v[2], sc.n_verts));
     Ray r2 = ray;
     r2.tmax = kInf;
     float t, b0, b1, b2;
@@ -456,9 +465,12 @@ __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const R
     float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
+    const pt_triangle trv = sc.tris[PT_IDX(idx, sc.n_tris)];
+    const V3 q0 = vload3(sc.P, PT_IDX(trv.v[0], sc.n_verts)), q1 = vload3(sc.P, PT_IDX(trv.v[1], sc.n_verts)),
+             q2 = vload3(sc.P, PT_IDX(trv.v[2], sc.n_verts));
     bool ok = (kSph && (flags & kPrimSphere)) ? sphere_surface(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, si)
               : (flags & kPrimPlane) ? plane_surface(sc.planes[PT_IDX(idx, sc.n_planes)], ray, si)
-                                     : tri_surface(sc, idx, ray, si);
+                                     : tri_surface(sc, idx, ray, si, q0, q1, q2);
     si->prim = prim;
     return ok;
 }
@@ -1190,7 +1202,9 @@ __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight&
         area = s.area;
     } else if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
         // Triangle::Intersect on this one triangle (tMax = Infinity).
-        ok = tri_surface(sc, l.shape, r, &isl);
+        const pt_triangle tr = sc.tris[PT_IDX(l.shape, sc.n_tris)];
+        ok = tri_surface(sc, l.shape, r, &isl, vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)),
+                         vload3(sc.P, PT_IDX(tr.v[1], sc.n_verts)), vload3(sc.P, PT_IDX(tr.v[2], sc.n_verts)));
     } else {
         ok = plane_surface(sc.planes[PT_IDX(l.shape, sc.n_planes)], r, &isl);
     }
