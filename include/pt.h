@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 7
+#define PT_ABI_VERSION 8
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -388,6 +388,11 @@ pt_status pt_render_range_accum(pt_scene* scene, int tile_offset, int tile_strid
  * for the hero integrators).  Batches beyond the 32-bit path-state indexing
  * limit (~252M slots; ~70M for hero scenes) are PT_ERR_INVALID_ARG. */
 pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
+
+/* Batches in flight (default 2): each pipeline is a host thread, a stream
+ * and its own path-state buffers; one batch's trace kernel overlaps another's
+ * shading.  1 runs the batches one after the other (isolated kernel timings). */
+pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
 
 /* Number of cropped pixels (rgb_out holds 3x this many floats). */
 pt_status pt_film_size(const pt_scene* scene, int32_t* width, int32_t* height);

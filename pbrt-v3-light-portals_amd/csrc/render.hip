@@ -7,6 +7,7 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -160,6 +161,8 @@ struct Frame {
     int height() const { return crop_y1 - crop_y0; }
 };
 
+constexpr int kMaxPipes = 4;  // render_tiles pipelines (PT_PIPES)
+
 struct Work {
     DBuf<uint32_t> hidx, st, rq0, rq1, pq0, pq1, counts;
     DBuf<float2> pfilm;
@@ -168,9 +171,33 @@ struct Work {
     DBuf<DevStats> stats;
     DBuf<int> dli;                 // DirectLighting state (kDl*)
     DBuf<float> dlf, dlframe;
-    size_t cap = 0;
+    DBuf<float> h_out60, h_L60, h_beta60, h_nee60, h_hs;  // hero integrators: 60-bin state per slot
+    size_t cap = 0, hero_cap = 0;
     int dl_frames = 0;             // > 0: DirectLighting buffers with this many frames per slot
-    void ensure(size_t n, size_t spill_threads, int frames) {
+    hipStream_t stream = nullptr;  // this pipeline's stream (render_tiles)
+    uint32_t* host_counts = nullptr;  // pinned: queue sizes read back per bounce
+    Work() = default;
+    Work(const Work&) = delete;
+    Work& operator=(const Work&) = delete;
+    ~Work() {
+        if (stream) (void)hipStreamDestroy(stream);
+        if (host_counts) (void)hipHostFree(host_counts);
+    }
+    void ensure(size_t n, size_t spill_threads, int frames, int hero_slots) {
+        if (!host_counts) {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+                throw PtError(PT_ERR_OOM, "hipHostMalloc failed");
+            host_counts = (uint32_t*)p;
+        }
+        if (hero_slots > 0 && (size_t)hero_slots > hero_cap) {
+            h_out60.alloc((size_t)hero_slots * kNSpec);
+            h_L60.alloc((size_t)hero_slots * kNSpec);
+            h_beta60.alloc((size_t)hero_slots * kNSpec);
+            h_nee60.alloc((size_t)hero_slots * kNSpec);
+            h_hs.alloc((size_t)hero_slots * kHs);
+            hero_cap = (size_t)hero_slots;
+        }
         if (frames > 0 && (n > cap || frames != dl_frames)) {
             dli.alloc((size_t)kDlInts * n);
             dlf.alloc((size_t)kDlFloats * n);
@@ -217,7 +244,7 @@ struct pt_scene {
     // hero integrators (SampledSpectrum scenes): tables, light distributions, per-slot radiance
     bool hero = false;
     pt::DevHero hh{};
-    pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist, h_out60, h_L60, h_beta60, h_nee60, h_hs;
+    pt::DBuf<float> h_xyz, h_illum, h_mat, h_light, h_wcdf, h_dist;
     pt::DBuf<int> h_matnb;
     pt::HaltonPixelConsts hpc{};
     pt::FilmConsts film{};
@@ -226,7 +253,8 @@ struct pt_scene {
     int spp = 0;
     std::vector<pt::LinearNode> host_nodes;
     std::vector<int> host_prim_order;
-    pt::Work work;
+    pt::Work work[pt::kMaxPipes];  // one set of path-state buffers per pipeline
+    int pipes = 2;                 // pipelines render_tiles runs batches on (PT_PIPES)
     int device = 0;
     int num_cus = 256;
     size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (8 M for the 60-bin hero state)
@@ -1042,61 +1070,85 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     dslot.upload(pixslot);
     const int maxBlocksTrace = s->num_cus * 16;
     const int maxBlocksShade = s->num_cus * 8;
-    Work& w = s->work;
     const bool direct = s->dev.integrator == PT_INTEGRATOR_DIRECT;
-    w.ensure(max_slots, (size_t)std::max(maxBlocksTrace, s->num_cus * s->trace_bpc) * kTraceBlock,
-             direct ? s->dev.dl_frames : 0);
-    HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), stream));
-    DevPaths ps = w.paths((int)max_slots);
-    DevHeroPaths hps{};
-    if (s->hero) {  // 60-bin radiance / throughput / pending light term + scalars per slot
-        s->h_out60.alloc(max_slots * (size_t)kNSpec);
-        s->h_L60.alloc(max_slots * (size_t)kNSpec);
-        s->h_beta60.alloc(max_slots * (size_t)kNSpec);
-        s->h_nee60.alloc(max_slots * (size_t)kNSpec);
-        s->h_hs.alloc(max_slots * (size_t)kHs);
-        s->hh.out60 = s->h_out60.p;
-        hps = DevHeroPaths{s->h_beta60.p, s->h_L60.p, s->h_nee60.p, s->h_hs.p};
+    // Batches run on `pipes` pipelines (host thread + stream + path-state
+    // buffers each), dealt round-robin: while one batch traces, another
+    // shades, so the latency-bound trace and shading kernels overlap on the
+    // device.  Each batch's film pass waits for the previous batch's (event
+    // chain): the FilmTiles are merged in the reference's tile order.
+    struct Batch { int g, s0; };
+    std::vector<Batch> batches;
+    for (int gi = 0; gi < (int)groups.size(); ++gi)
+        for (int s0 = s_begin; s0 < s_end; s0 += groups[gi].S) batches.push_back({gi, s0});
+    const int pipes = std::max(1, std::min({s->pipes, kMaxPipes, (int)batches.size()}));
+    for (int k = 0; k < pipes; ++k) {
+        Work& w = s->work[k];
+        HIPCHK(hipSetDevice(s->device));
+        w.ensure(max_slots, (size_t)std::max(maxBlocksTrace, s->num_cus * s->trace_bpc) * kTraceBlock,
+                 direct ? s->dev.dl_frames : 0, s->hero ? (int)max_slots : 0);
+        if (!w.stream) HIPCHK(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+        HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), w.stream));
     }
-    hipEvent_t ev0, ev1;
-    HIPCHK(hipEventCreate(&ev0));
-    HIPCHK(hipEventCreate(&ev1));
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
-    auto tev_get = [&](size_t i) {
-        while (tev.size() <= i) {
-            hipEvent_t a, b;
-            HIPCHK(hipEventCreate(&a));
-            HIPCHK(hipEventCreate(&b));
-            tev.push_back({a, b});
-        }
-        return tev[i];
-    };
-    double trace_ms = 0, shade_ms = 0;
-    size_t tcount = 0;
-    std::vector<size_t> shade_ev;  // tev indices of the shading launches
+    // the caller's stream has everything before this call (e.g. the film clear)
+    {
+        hipEvent_t e0;
+        HIPCHK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(e0, stream));
+        for (int k = 0; k < pipes; ++k) HIPCHK(hipStreamWaitEvent(s->work[k].stream, e0, 0));
+        HIPCHK(hipStreamSynchronize(stream));
+        (void)hipEventDestroy(e0);
+    }
+    std::vector<hipEvent_t> film_done(batches.size());
+    for (auto& e : film_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<char> film_recorded(batches.size(), 0);
     // PT_SYNC_CHECK=1 (diagnostics): synchronise after every launch so a
     // device fault is reported against the kernel and bounce that raised it.
     const bool syncCheck = std::getenv("PT_SYNC_CHECK") != nullptr;
-    auto sync_check = [&](const char* what, int it) {
-        if (!syncCheck) return;
-        const hipError_t e = hipStreamSynchronize(stream);
-        if (e != hipSuccess)
-            throw PtError(PT_ERR_DEVICE, std::string(what) + " (bounce iteration " + std::to_string(it) + "): " +
-                                             hipGetErrorString(e));
-    };
-    HIPCHK(hipEventRecord(ev0, stream));
-    uint32_t* counts = w.counts.p;
-    uint32_t host_counts[8];
-    for (const Group& g : groups) {
-        for (int s0 = s_begin; s0 < s_end; s0 += g.S) {
+    struct PipeTiming { double trace_ms = 0, shade_ms = 0; uint64_t launches = 0, shade_launches = 0, samples = 0; };
+    std::vector<PipeTiming> pt(pipes);
+    std::vector<std::exception_ptr> err(pipes);
+    auto run_pipe = [&](int k) {
+        Work& w = s->work[k];
+        hipStream_t st = w.stream;
+        HIPCHK(hipSetDevice(s->device));
+        DevPaths ps = w.paths((int)max_slots);
+        DevHeroPaths hps{};
+        DevHero hh = s->hh;
+        if (s->hero) {
+            hh.out60 = w.h_out60.p;
+            hps = DevHeroPaths{w.h_beta60.p, w.h_L60.p, w.h_nee60.p, w.h_hs.p};
+        }
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+        std::vector<char> is_shade;
+        auto tev_new = [&](bool shade) {
+            hipEvent_t e0, e1;
+            HIPCHK(hipEventCreate(&e0));
+            HIPCHK(hipEventCreate(&e1));
+            tev.push_back({e0, e1});
+            is_shade.push_back(shade ? 1 : 0);
+            return tev.back();
+        };
+        auto sync_check = [&](const char* what, int it) {
+            if (!syncCheck) return;
+            const hipError_t e = hipStreamSynchronize(st);
+            if (e != hipSuccess)
+                throw PtError(PT_ERR_DEVICE, std::string(what) + " (bounce iteration " + std::to_string(it) + "): " +
+                                                 hipGetErrorString(e));
+        };
+        uint32_t* counts = w.counts.p;
+        for (size_t bi = (size_t)k; bi < batches.size(); bi += (size_t)pipes) {
+            const Group& g = groups[batches[bi].g];
+            const int s0 = batches[bi].s0;
             const int ns = std::min(g.S, s_end - s0);
             const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
             hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
-                               stream, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
+                               st, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
             if (s->hero)  // the hero wavelengths and 60-bin path state of every camera sample
                 hipLaunchKernelGGL(k_hero_init, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))),
-                                   dim3(256), 0, stream, s->dev, s->hh, ps, hps, nb);
-            hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nb, nb);
+                                   dim3(256), 0, st, s->dev, hh, ps, hps, nb);
+            hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, counts, nb, nb);
             HIPCHK(hipGetLastError());
             sync_check("k_camera", 0);
             uint32_t *rq_in = w.rq0.p, *rq_out = w.rq1.p, *pq_in = w.pq0.p, *pq_out = w.pq1.p;
@@ -1105,96 +1157,135 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             while (npaths > 0) {
                 // counts[0]/[1] hold the input sizes, [2]/[3] the output sizes
                 if (nrays > 0) {
-                    auto e = tev_get(tcount++);
-                    HIPCHK(hipEventRecord(e.first, stream));
+                    auto e = tev_new(false);
+                    HIPCHK(hipEventRecord(e.first, st));
                     const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
                     if (s->trace_persist == 2 && !s->trace_spill) {
                         // branch-reduced persistent traversal; LDS stack of depth+1 rows
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
                         hipLaunchKernelGGL(trace_nb_kernel(s->lds_scene_bytes != 0, s->has_spheres), pg,
-                                           dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0, counts + 4,
+                                           dim3(kTraceBlock), lds, st, s->dev, ps, rq_in, counts + 0, counts + 4,
                                            s->refill_min, s->leaf_min, w.stats.p);
                     } else if (s->trace_persist) {
                         // persistent: about one resident wave set; lanes refill from counts[4]
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
                         const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
-                        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, stream, s->dev, ps, rq_in, counts + 0,
+                        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq_in, counts + 0,
                                            counts + 4, s->refill_min, s->leaf_min_pt, s->stack_rows, w.spill.p,
                                            w.stats.p);
                     } else if (s->lds_scene_bytes)
-                        hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes, stream, s->dev,
-                                           ps, rq_in, counts + 0, w.spill.p, w.stats.p);
+                        hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes,
+                                           st, s->dev, ps, rq_in, counts + 0, w.spill.p, w.stats.p);
                     else
-                        hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, stream, s->dev, ps, rq_in,
-                                           counts + 0, w.spill.p, w.stats.p);
-                    HIPCHK(hipEventRecord(e.second, stream));
-                    rr.launches++;
+                        hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, st, s->dev,
+                                           ps, rq_in, counts + 0, w.spill.p, w.stats.p);
+                    HIPCHK(hipEventRecord(e.second, st));
+                    pt[k].launches++;
                     sync_check("k_trace", iter);
                 }
                 const dim3 sg(std::max(1, std::min(ceil_div(npaths, kShadeBlock), maxBlocksShade)));
-                const size_t sev = tcount++;
-                shade_ev.push_back(sev);
-                HIPCHK(hipEventRecord(tev_get(sev).first, stream));
+                auto es = tev_new(true);
+                HIPCHK(hipEventRecord(es.first, st));
                 if (s->hero) {
-                    hipLaunchKernelGGL(s->hero_waves == 1 ? k_shade_hero : (s->hero_waves == 2 ? k_shade_hero_w2 : k_shade_hero_w4), sg, dim3(kShadeBlock), 0, stream, s->dev, s->hh, ps, hps, pq_in,
-                                       counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
+                    hipLaunchKernelGGL(s->hero_waves == 1 ? k_shade_hero : (s->hero_waves == 2 ? k_shade_hero_w2 : k_shade_hero_w4),
+                                       sg, dim3(kShadeBlock), 0, st, s->dev, hh, ps, hps, pq_in, counts + 1, rq_out,
+                                       counts + 2, pq_out, counts + 3, w.stats.p);
                 } else {
                     const ShadeKernel kshade =
                         direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
-                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, stream, s->dev, ps, pq_in, counts + 1,
+                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, st, s->dev, ps, pq_in, counts + 1,
                                        rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(tev_get(sev).second, stream));
+                HIPCHK(hipEventRecord(es.second, st));
+                pt[k].shade_launches++;
                 sync_check("k_shade", iter);
-                HIPCHK(hipMemcpyAsync(host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-                HIPCHK(hipStreamSynchronize(stream));
-                nrays = host_counts[0];
-                npaths = host_counts[1];
-                hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, stream, counts, nrays, npaths);
+                HIPCHK(hipMemcpyAsync(w.host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                nrays = w.host_counts[0];
+                npaths = w.host_counts[1];
+                hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, counts, nrays, npaths);
                 std::swap(rq_in, rq_out);
                 std::swap(pq_in, pq_out);
                 if (++iter > 100000) throw PtError(PT_ERR_STATE, "path loop did not terminate");
+            }
+            if (bi > 0) {  // FilmTiles merge in batch (tile) order
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return film_recorded[bi - 1] != 0; });
+                lk.unlock();
+                HIPCHK(hipStreamWaitEvent(st, film_done[bi - 1], 0));
             }
             const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
             if (bw > 0 && bh > 0) {
                 const dim3 fg(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32)));
                 if (s->hero)
-                    hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, stream, s->hh, ps, s->film, dslot.p, g.p0, g.np,
+                    hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, st, hh, ps, s->film, dslot.p, g.p0, g.np,
                                        ns, g.bx0, g.by0, bw, bh, d_accum);
                 else
-                    hipLaunchKernelGGL(k_film, fg, dim3(256), 0, stream, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0,
+                    hipLaunchKernelGGL(k_film, fg, dim3(256), 0, st, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0,
                                        g.by0, bw, bh, d_accum);
                 HIPCHK(hipGetLastError());
                 sync_check("k_film", 0);
             }
-            rr.samples += nb;
+            HIPCHK(hipEventRecord(film_done[bi], st));
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                film_recorded[bi] = 1;
+            }
+            cv.notify_all();
+            pt[k].samples += nb;
         }
+        HIPCHK(hipStreamSynchronize(st));
+        for (size_t i = 0; i < tev.size(); ++i) {
+            float t = 0;
+            HIPCHK(hipEventElapsedTime(&t, tev[i].first, tev[i].second));
+            (is_shade[i] ? pt[k].shade_ms : pt[k].trace_ms) += t;
+            (void)hipEventDestroy(tev[i].first);
+            (void)hipEventDestroy(tev[i].second);
+        }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        std::vector<std::thread> th;
+        for (int k = 1; k < pipes; ++k)
+            th.emplace_back([&, k] {
+                try {
+                    run_pipe(k);
+                } catch (...) {
+                    err[k] = std::current_exception();
+                    std::lock_guard<std::mutex> lk(mu);  // release waiters: mark this pipe's batches done
+                    for (size_t bi = (size_t)k; bi < batches.size(); bi += (size_t)pipes) film_recorded[bi] = 1;
+                    cv.notify_all();
+                }
+            });
+        try {
+            run_pipe(0);
+        } catch (...) {
+            err[0] = std::current_exception();
+            std::lock_guard<std::mutex> lk(mu);
+            for (size_t bi = 0; bi < batches.size(); bi += (size_t)pipes) film_recorded[bi] = 1;
+            cv.notify_all();
+        }
+        for (auto& t : th) t.join();
     }
-    HIPCHK(hipEventRecord(ev1, stream));
-    HIPCHK(hipMemcpyAsync(&rr.st, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
-    rr.render_ms = ms;
-    std::vector<char> is_shade(tcount, 0);
-    for (size_t i : shade_ev) is_shade[i] = 1;
-    for (size_t i = 0; i < tcount; ++i) {
-        float t = 0;
-        HIPCHK(hipEventElapsedTime(&t, tev[i].first, tev[i].second));
-        (is_shade[i] ? shade_ms : trace_ms) += t;
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    rr.render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (auto& e : film_done) (void)hipEventDestroy(e);
+    for (int k = 0; k < pipes; ++k) {
+        DevStats d{};
+        HIPCHK(hipMemcpy(&d, s->work[k].stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+        rr.st.closest += d.closest; rr.st.shadow += d.shadow; rr.st.nodes += d.nodes; rr.st.prims += d.prims;
+        rr.st.dim_overflow += d.dim_overflow; rr.st.lane_iters += d.lane_iters; rr.st.lane_steps += d.lane_steps;
+        rr.st.shade_bytes += d.shade_bytes;
+        rr.trace_ms += pt[k].trace_ms;
+        rr.shade_ms += pt[k].shade_ms;
+        rr.launches += pt[k].launches;
+        rr.shade_launches += pt[k].shade_launches;
+        rr.samples += pt[k].samples;
     }
-    rr.trace_ms = trace_ms;
-    rr.shade_ms = shade_ms;
-    rr.shade_launches = shade_ev.size();
-    for (auto& e : tev) {
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
-    }
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
     if (rr.st.dim_overflow) throw PtError(PT_ERR_UNSUPPORTED, "Halton dimension table exhausted");
 #ifdef PT_GUARDS
     unsigned int guard = 0;
@@ -1352,6 +1443,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN_PT")) s->leaf_min_pt = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("PT_PIPES")) s->pipes = std::max(1, std::min(kMaxPipes, std::atoi(t)));
     return s;
 }
 
@@ -1682,6 +1774,14 @@ pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
             throw PtError(PT_ERR_INVALID_ARG, "batch slots exceed the 32-bit path-state indexing limit (" +
                                                   std::to_string(slot_limit(s)) + ")");
         s->target_slots = (size_t)slots;
+    });
+}
+
+pt_status pt_set_pipelines(pt_scene* s, int32_t pipelines) {
+    return guarded([&] {
+        if (!s || pipelines < 1 || pipelines > kMaxPipes) throw PtError(PT_ERR_INVALID_ARG, "pipelines must be in [1, 4]");
+        s->pipes = pipelines;
+        for (auto& r : s->replicas) r->pipes = pipelines;
     });
 }
 

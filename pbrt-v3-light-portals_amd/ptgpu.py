@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
     L.pt_resolve_film_host.argtypes = [vp, f32p, f32p]
     L.pt_film_size_host.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_set_batch_slots.argtypes = [vp, ctypes.c_int64]
+    L.pt_set_pipelines.argtypes = [vp, ctypes.c_int32]
     L.pt_write_pfm.argtypes = [ctypes.c_char_p, f32p, i32, i32]
     L.pt_write_image.argtypes = [ctypes.c_char_p, f32p, i32, i32, i32, i32, i32, i32]
     L.pt_write_film_image.argtypes = [vp, ctypes.c_char_p, f32p]
@@ -306,6 +307,10 @@ class Scene:
         _check(lib().pt_scene_create(host.desc, ctypes.byref(self._s)))
         if batch_slots:
             _check(lib().pt_set_batch_slots(self._s, int(batch_slots)))
+
+    def set_pipelines(self, n: int) -> None:
+        """pt_set_pipelines: batches in flight (1 = one after the other)."""
+        _check(lib().pt_set_pipelines(self._s, int(n)))
 
     @property
     def handle(self) -> int:
