@@ -659,6 +659,10 @@ struct Bsdf {
     float eta;             // BSDF::eta
     const pt_material* m;
     V3 ns, ng, ss, ts;
+    // the material's constant Kd / Kr / Kt, held by value: the hero
+    // integrators overwrite them per 3-bin chunk of the 60-bin reflectances
+    // (a private material copy behind `m` would live in scratch)
+    S3 rkd, rkr, rkt;
 };
 
 __device__ __forceinline__ V3 refl_z(V3 wo) { return v3(-wo.x, -wo.y, wo.z); }
@@ -692,7 +696,7 @@ __device__ __forceinline__ S3 mfrefl_R(const Bsdf& b) {
     const pt_material* m = b.m;
     if (m->kind == PT_MAT_METAL) return s3(1.f);
     if (m->kind == PT_MAT_PLASTIC) return clamp0(s3(m->ks[0], m->ks[1], m->ks[2]));
-    return clamp0(s3(m->kr[0], m->kr[1], m->kr[2]));
+    return clamp0(b.rkr);
 }
 __device__ __forceinline__ S3 mfrefl_F(const Bsdf& b, float cosThetaI) {
     const pt_material* m = b.m;
@@ -728,8 +732,7 @@ __device__ __forceinline__ S3 mftrans_f(const Bsdf& b, V3 wo, V3 wi) {
     const float ax = b.m->alpha[0], ay = b.m->alpha[1];
     const float v = fabsf(tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) *
                           factor * factor / (cosI * cosO * sqrtDenom * sqrtDenom));
-    const pt_material* m = b.m;
-    return ((s3(1.f) - F) * clamp0(s3(m->kt[0], m->kt[1], m->kt[2]))) * v;
+    return ((s3(1.f) - F) * clamp0(b.rkt)) * v;
 }
 __device__ __forceinline__ float mftrans_pdf(const Bsdf& b, V3 wo, V3 wi) {
     if (wo.z * wi.z > 0) return 0;
@@ -740,18 +743,20 @@ __device__ __forceinline__ float mftrans_pdf(const Bsdf& b, V3 wo, V3 wi) {
     const float dwh_dwi = fabsf((eta * eta * dot(wi, wh)) / (sqrtDenom * sqrtDenom));
     return tr_pdf(b.m->alpha[0], b.m->alpha[1], wo, wh) * dwh_dwi;
 }
-__device__ __forceinline__ S3 lambert_R(const Bsdf& b) { return clamp0(s3(b.m->kd[0], b.m->kd[1], b.m->kd[2])); }
+__device__ __forceinline__ S3 lambert_R(const Bsdf& b) { return clamp0(b.rkd); }
 
 template <int kFt = kFtAll>
 __device__ __forceinline__ S3 lobe_f(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::f
-    if (!Ft<kFt>::micro || k == kLbLambert) return lambert_R(b) * kInvPi;
+    if (k == kLbLambert || !(Ft<kFt>::micro || Ft<kFt>::spec)) return lambert_R(b) * kInvPi;
+    if (!Ft<kFt>::micro) return s3(0.f);  // specular lobes: f = 0
     if (k == kLbMfRefl) return mfrefl_f(b, wo, wi);
     if (k == kLbMfTrans) return mftrans_f(b, wo, wi);
     return s3(0.f);
 }
 template <int kFt = kFtAll>
 __device__ __forceinline__ float lobe_pdf(const Bsdf& b, int k, V3 wo, V3 wi) {  // BxDF::Pdf
-    if (!Ft<kFt>::micro || k == kLbLambert) return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    if (k == kLbLambert || !(Ft<kFt>::micro || Ft<kFt>::spec)) return (wo.z * wi.z > 0) ? fabsf(wi.z) * kInvPi : 0;
+    if (!Ft<kFt>::micro) return 0.f;  // specular lobes: pdf = 0
     if (k == kLbMfRefl) {
         if (!(wo.z * wi.z > 0)) return 0.f;
         const V3 wh = normalize(wo + wi);
@@ -792,12 +797,12 @@ __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, f
     if (k == kLbSpecRefl) {  // SpecularReflection::Sample_f, FresnelNoOp
         *wi = refl_z(wo);
         *pdf = 1;
-        return (s3(1.f) * clamp0(s3(m->kr[0], m->kr[1], m->kr[2]))) / fabsf(wi->z);
+        return (s3(1.f) * clamp0(b.rkr)) / fabsf(wi->z);
     }
     if (k == kLbSpecReflD) {  // SpecularReflection::Sample_f (reflection.h:400-410), FresnelDielectric(1, eta)
         *wi = refl_z(wo);
         *pdf = 1;
-        return (s3(fr_dielectric(wi->z, 1.f, b.eta)) * clamp0(s3(m->kr[0], m->kr[1], m->kr[2]))) / fabsf(wi->z);
+        return (s3(fr_dielectric(wi->z, 1.f, b.eta)) * clamp0(b.rkr)) / fabsf(wi->z);
     }
     if (k == kLbSpecTrans) {  // SpecularTransmission::Sample_f (reflection.cpp:183-199), etaA = 1, etaB = eta
         const bool entering = wo.z > 0;
@@ -806,7 +811,7 @@ __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, f
         const V3 n = dot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1);  // Faceforward(n, wo)
         if (!refract(wo, n, etaI / etaT, wi)) return s3(0.f);
         *pdf = 1;
-        S3 ft = clamp0(s3(m->kt[0], m->kt[1], m->kt[2])) * (s3(1.f) - s3(fr_dielectric(wi->z, 1.f, b.eta)));
+        S3 ft = clamp0(b.rkt) * (s3(1.f) - s3(fr_dielectric(wi->z, 1.f, b.eta)));
         ft = ft * ((etaI * etaI) / (etaT * etaT));  // TransportMode::Radiance
         return ft / fabsf(wi->z);
     }
@@ -816,14 +821,14 @@ __device__ __forceinline__ S3 lobe_sample(const Bsdf& b, int k, V3 wo, V3* wi, f
         *wi = refl_z(wo);
         *type = kBxSpecular | kBxR;
         *pdf = F;
-        return (clamp0(s3(m->kr[0], m->kr[1], m->kr[2])) * F) / fabsf(wi->z);
+        return (clamp0(b.rkr) * F) / fabsf(wi->z);
     }
     const bool entering = wo.z > 0;
     const float etaI = entering ? 1.f : b.eta;
     const float etaT = entering ? b.eta : 1.f;
     const V3 n = dot(v3(0, 0, 1), wo) < 0.f ? v3(0, 0, -1) : v3(0, 0, 1);  // Faceforward(n, wo)
     if (!refract(wo, n, etaI / etaT, wi)) return s3(0.f);
-    S3 ft = clamp0(s3(m->kt[0], m->kt[1], m->kt[2])) * (1 - F);
+    S3 ft = clamp0(b.rkt) * (1 - F);
     ft = ft * ((etaI * etaI) / (etaT * etaT));  // TransportMode::Radiance
     *type = kBxSpecular | kBxT;
     *pdf = 1 - F;
@@ -845,6 +850,9 @@ __device__ __forceinline__ void make_bsdf(const pt_material* m, const SurfHit& s
     b->ss = normalize(si.sdpdu);
     b->ts = cross(b->ns, b->ss);
     b->m = m;
+    b->rkd = s3(m->kd[0], m->kd[1], m->kd[2]);
+    b->rkr = s3(m->kr[0], m->kr[1], m->kr[2]);
+    b->rkt = s3(m->kt[0], m->kt[1], m->kt[2]);
     b->n = 0;
     b->lk0 = b->lk1 = 0;
     b->eta = 1;

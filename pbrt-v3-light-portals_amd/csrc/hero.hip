@@ -27,7 +27,11 @@ constexpr int kNS = 60;
 // The 60-bin loops over the bin-major state run in groups of kG bins: a
 // group's loads are all issued before its stores (the arrays may alias, so
 // the compiler cannot move a load above an earlier store itself).
-constexpr int kG = 12;
+#ifndef PT_HERO_G
+#define PT_HERO_G 12
+#endif
+constexpr int kG = PT_HERO_G;  // 3, 6 or 12 (whole 3-bin chunks)
+static_assert(kNS % kG == 0 && kG % 3 == 0, "bin groups hold whole chunks");
 __device__ __forceinline__ void gload(const float* g, uint32_t N, int i0, float* r) {
 #pragma unroll
     for (int j = 0; j < kG; ++j) r[j] = g[(uint32_t)(i0 + j) * N];
@@ -53,6 +57,7 @@ struct DevHero {
     V3 wb_min, wb_max;       // scene.WorldBound()
     int mis;                 // hero_path_mis (else hero_path)
     float* out60;            // per batch slot: the sample's 60-bin radiance
+    float* out_y;            // per batch slot: its L.y(), -inf if a bin is NaN (k_film_s60's sanitiser input)
 };
 
 __device__ __forceinline__ float s60_y(const DevHero& h, const float* c) {  // spectrum.h:407-413
@@ -60,124 +65,233 @@ __device__ __forceinline__ float s60_y(const DevHero& h, const float* c) {  // s
     for (int i = 0; i < kNS; ++i) yy += h.XYZ[kNS + i] * c[i];
     return yy * (float)(700 - 400) / (float)(106.856895f * kNS);
 }
-// SampledSpectrum::FromRGB(rgb, Illuminant) (spectrum.cpp:136-172)
-__device__ __forceinline__ void s60_from_rgb_illum(const DevHero& h, S3 rgb, float* r) {
-    for (int i = 0; i < kNS; ++i) r[i] = 0.f;
-    auto add = [&](float a, int k) {
-        for (int i = 0; i < kNS; ++i) r[i] += h.illum[k * kNS + i] * a;
-    };
+// SampledSpectrum::FromRGB(rgb, Illuminant) (spectrum.cpp:136-172), one bin
+// at a time: the reference's branch picks three basis spectra (W C M Y R G B)
+// and weights; bin i is then its elementwise ops in the same order
+struct RgbIllum {
+    float a[3];
+    int k[3];
+};
+__device__ __forceinline__ RgbIllum rgb_illum(S3 rgb) {
     const float c0 = rgb.c[0], c1 = rgb.c[1], c2 = rgb.c[2];
-    if (c0 <= c1 && c0 <= c2) {
-        add(c0, 0);
-        if (c1 <= c2) { add(c1 - c0, 1); add(c2 - c1, 6); }
-        else { add(c2 - c0, 1); add(c1 - c2, 5); }
-    } else if (c1 <= c0 && c1 <= c2) {
-        add(c1, 0);
-        if (c0 <= c2) { add(c0 - c1, 2); add(c2 - c0, 6); }
-        else { add(c2 - c1, 2); add(c0 - c2, 4); }
-    } else {
-        add(c2, 0);
-        if (c0 <= c1) { add(c0 - c2, 3); add(c1 - c0, 5); }
-        else { add(c1 - c2, 3); add(c0 - c1, 4); }
-    }
-    for (int i = 0; i < kNS; ++i) {
-        float v = r[i] * .86445f;
-        r[i] = v < 0 ? 0.f : (v > kInf ? kInf : v);  // Clamp(0, Infinity)
-    }
+    auto mk = [](float a0, int k0, float a1, int k1, float a2, int k2) { return RgbIllum{{a0, a1, a2}, {k0, k1, k2}}; };
+    if (c0 <= c1 && c0 <= c2)
+        return c1 <= c2 ? mk(c0, 0, c1 - c0, 1, c2 - c1, 6) : mk(c0, 0, c2 - c0, 1, c1 - c2, 5);
+    if (c1 <= c0 && c1 <= c2)
+        return c0 <= c2 ? mk(c1, 0, c0 - c1, 2, c2 - c0, 6) : mk(c1, 0, c2 - c1, 2, c0 - c2, 4);
+    return c0 <= c1 ? mk(c2, 0, c0 - c2, 3, c1 - c0, 5) : mk(c2, 0, c1 - c2, 3, c0 - c1, 4);
+}
+__device__ __forceinline__ float rgb_illum_bin(const DevHero& h, const RgbIllum& c, int i) {
+    float r = 0.f;
+    r += h.illum[c.k[0] * kNS + i] * c.a[0];
+    r += h.illum[c.k[1] * kNS + i] * c.a[1];
+    r += h.illum[c.k[2] * kNS + i] * c.a[2];
+    const float v = r * .86445f;
+    return v < 0 ? 0.f : (v > kInf ? kInf : v);  // Clamp(0, Infinity)
+}
+__device__ __forceinline__ void s60_from_rgb_illum(const DevHero& h, S3 rgb, float* r) {
+    const RgbIllum c = rgb_illum(rgb);
+    for (int i = 0; i < kNS; ++i) r[i] = rgb_illum_bin(h, c, i);
 }
 __device__ __forceinline__ float s60_y_zero() {  // Spectrum(0).y()
     return 0.f * (float)(700 - 400) / (float)(106.856895f * kNS);
-}
-__device__ __forceinline__ bool s60_black(const float* c) {
-    for (int i = 0; i < kNS; ++i)
-        if (c[i] != 0.f) return false;
-    return true;
 }
 
 // the 60-bin BSDF of a surface: the lobe set from a representative material,
 // values per 3-bin chunk from a material copy holding that chunk's reflectances
 struct HeroBsdf {
-    Bsdf b;
-    pt_material rep;  // lobe-selection stand-in; chunk values are written into it
+    Bsdf b;    // lobes from a representative material; b.rkd / rkr / rkt hold the current 3-bin chunk
     int mi;
+    int kind;  // the representative's kind (dispersive glass -> glass with the hero eta)
 };
+template <int kFt>
 __device__ __forceinline__ void hb_make(const DevScene& sc, const DevHero& h, int mi, const SurfHit& si, float eta,
                                         HeroBsdf* hb) {
-    hb->rep = sc.mats[PT_IDX(mi, sc.n_mats)];
+    pt_material rep = sc.mats[PT_IDX(mi, sc.n_mats)];  // lobe-selection stand-in
     hb->mi = mi;
     const int nb = h.mat_nb[mi];
     const float one = (nb & 1) ? 1.f : 0.f, r = (nb & 2) ? 1.f : 0.f, t = (nb & 4) ? 1.f : 0.f;
-    for (int c = 0; c < 3; ++c) { hb->rep.kd[c] = one; hb->rep.kr[c] = r; hb->rep.kt[c] = t; }
-    if (hb->rep.kind == PT_MAT_DISPERSIVE_GLASS) { hb->rep.kind = PT_MAT_GLASS; hb->rep.ior = eta; }
-    make_bsdf<kFtAll>(&hb->rep, si, 550.f, &hb->b);
-    hb->b.m = &hb->rep;
+    for (int c = 0; c < 3; ++c) { rep.kd[c] = one; rep.kr[c] = r; rep.kt[c] = t; }
+    if (rep.kind == PT_MAT_DISPERSIVE_GLASS) { rep.kind = PT_MAT_GLASS; rep.ior = eta; }
+    make_bsdf<kFt>(&rep, si, 550.f, &hb->b);
+    hb->b.m = &sc.mats[PT_IDX(mi, sc.n_mats)];  // lobes read only kind / ks / eta / k / alpha through it
+    hb->kind = rep.kind;
 }
 __device__ __forceinline__ void hb_chunk(const DevHero& h, HeroBsdf* hb, int k) {
     const float* ms = h.mat_s60 + (size_t)hb->mi * 3 * kNS;
-    for (int c = 0; c < 3; ++c) {
-        hb->rep.kd[c] = ms[3 * k + c];
-        hb->rep.kr[c] = ms[kNS + 3 * k + c];
-        hb->rep.kt[c] = ms[2 * kNS + 3 * k + c];
-    }
-}
-__device__ __forceinline__ void hb_f(const DevHero& h, HeroBsdf* hb, V3 wo, V3 wi, float* f) {
-    for (int k = 0; k < kNS / 3; ++k) {
-        hb_chunk(h, hb, k);
-        const S3 v = bsdf_f<kFtAll>(hb->b, wo, wi, kBxAll);
-        f[3 * k] = v.c[0]; f[3 * k + 1] = v.c[1]; f[3 * k + 2] = v.c[2];
-    }
+    hb->b.rkd = s3(ms[3 * k], ms[3 * k + 1], ms[3 * k + 2]);
+    hb->b.rkr = s3(ms[kNS + 3 * k], ms[kNS + 3 * k + 1], ms[kNS + 3 * k + 2]);
+    hb->b.rkt = s3(ms[2 * kNS + 3 * k], ms[2 * kNS + 3 * k + 1], ms[2 * kNS + 3 * k + 2]);
 }
 // 12 bins of the spectra the material kind reads (Kd: matte; Kr, Kt: glass;
 // Kr: mirror; all three otherwise), as 16-byte loads, and chunk c of them
 // written into the material copy.
 struct HbGroup {
-    float4 v[3][kG / 4];
+    float v[3][kG];
 };
 __device__ __forceinline__ void hb_group(const DevHero& h, const HeroBsdf* hb, int i0, HbGroup* g) {
-    const int kind = hb->rep.kind;
+    const int kind = hb->kind;
     const int use = kind == PT_MAT_MATTE ? 1 : (kind == PT_MAT_GLASS ? 6 : (kind == PT_MAT_MIRROR ? 2 : 7));
-    const float4* ms = (const float4*)(h.mat_s60 + (size_t)hb->mi * 3 * kNS + i0);
+    const float* ms = h.mat_s60 + (size_t)hb->mi * 3 * kNS + i0;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int q = 0; q < kG / 4; ++q) g->v[j][q] = (use >> j & 1) ? ms[j * kNS / 4 + q] : make_float4(0, 0, 0, 0);
+        for (int q = 0; q < kG; ++q) g->v[j][q] = (use >> j & 1) ? ms[j * kNS + q] : 0.f;
 }
-__device__ __forceinline__ float g_at(const HbGroup& g, int j, int b) {
-    const float4 v = g.v[j][b / 4];
-    const int r = b % 4;
-    return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
-}
+__device__ __forceinline__ float g_at(const HbGroup& g, int j, int b) { return g.v[j][b]; }
 __device__ __forceinline__ void hb_chunk_g(HeroBsdf* hb, const HbGroup& g, int c) {
-    for (int q = 0; q < 3; ++q) {
-        hb->rep.kd[q] = g_at(g, 0, 3 * c + q);
-        hb->rep.kr[q] = g_at(g, 1, 3 * c + q);
-        hb->rep.kt[q] = g_at(g, 2, 3 * c + q);
-    }
+    hb->b.rkd = s3(g_at(g, 0, 3 * c), g_at(g, 0, 3 * c + 1), g_at(g, 0, 3 * c + 2));
+    hb->b.rkr = s3(g_at(g, 1, 3 * c), g_at(g, 1, 3 * c + 1), g_at(g, 1, 3 * c + 2));
+    hb->b.rkt = s3(g_at(g, 2, 3 * c), g_at(g, 2, 3 * c + 1), g_at(g, 2, 3 * c + 2));
 }
+template <int kFt>
 __device__ __forceinline__ float hb_f1(const DevHero& h, HeroBsdf* hb, V3 wo, V3 wi, int bin) {
     hb_chunk(h, hb, bin / 3);
-    return bsdf_f<kFtAll>(hb->b, wo, wi, kBxAll).c[bin % 3];
+    return bsdf_f<kFt>(hb->b, wo, wi, kBxAll).c[bin % 3];
 }
 
 // The lobe sum of BSDF::f (reflection.cpp:713-726) for local directions and
 // a fixed reflect test, at the chunk the material copy currently holds.
+template <int kFt>
 __device__ __forceinline__ S3 hb_lobes_f(const Bsdf& b, V3 wo, V3 wi, bool reflect) {
     S3 f = s3(0.f);
-    for (int i = 0; i < Ft<kFtAll>::max_lobes; ++i) {
+    for (int i = 0; i < Ft<kFt>::max_lobes; ++i) {
         if (i >= b.n) break;
         const int k = lobe_at(b, i), t = lobe_type(k);
         if (lobe_matches(k, kBxAll) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT))))
-            f = f + lobe_f<kFtAll>(b, k, wo, wi);
+            f = f + lobe_f<kFt>(b, k, wo, wi);
     }
     return f;
 }
+// A lobe's value at fixed local directions with the chunk's reflectance
+// factored out: f_c = (((clamp0(X)_c * a) * b) * c) / d is the per-channel
+// operation chain of lobe_f / lobe_sample (devfuncs.h) for every lobe of the
+// hero materials (x * 1 and x / 1 are exact, so shorter chains pad with
+// ones).  The direction-only part (D, G, Fresnel, cosines) is computed once
+// per vertex instead of once per 3-bin chunk.  src: 0 Kd, 1 Kr, 2 Kt, -1 a
+// lobe that returned black.
+struct LobeTerm {
+    int src;
+    float a, b, c, d;
+};
+struct HbTerms {
+    LobeTerm t[2];
+    int n;
+    bool generic;  // metal / plastic microfacet lobes: evaluate per chunk (hb_lobes_f)
+};
+__device__ __forceinline__ LobeTerm lobe_term(int src, float a, float b = 1.f, float c = 1.f, float d = 1.f) {
+    return LobeTerm{src, a, b, c, d};
+}
+template <int kFt>
+__device__ __forceinline__ LobeTerm lobe_f_term(const Bsdf& b, int k, V3 wo, V3 wi) {  // lobe_f
+    const LobeTerm black = lobe_term(-1, 0.f);
+    if (k == kLbLambert || !(Ft<kFt>::micro || Ft<kFt>::spec)) return lobe_term(0, kInvPi);
+    if (!Ft<kFt>::micro) return black;  // specular lobes: f = 0
+    const float ax = b.m->alpha[0], ay = b.m->alpha[1];
+    if (k == kLbMfRefl) {  // mfrefl_f, dielectric Fresnel
+        const float cosO = fabsf(wo.z), cosI = fabsf(wi.z);
+        V3 wh = wi + wo;
+        if (cosI == 0 || cosO == 0) return black;
+        if (wh.x == 0 && wh.y == 0 && wh.z == 0) return black;
+        wh = normalize(wh);
+        const V3 whf = dot(wh, v3(0, 0, 1)) < 0.f ? -wh : wh;
+        const float F = fr_dielectric(dot(wi, whf), 1.f, b.eta);
+        return lobe_term(1, tr_D(ax, ay, wh), tr_G(ax, ay, wo, wi), F, 4 * cosI * cosO);
+    }
+    if (k == kLbMfTrans) {  // mftrans_f
+        if (wo.z * wi.z > 0) return black;
+        const float cosO = wo.z, cosI = wi.z;
+        if (cosI == 0 || cosO == 0) return black;
+        const float eta = wo.z > 0 ? (b.eta / 1.f) : (1.f / b.eta);
+        V3 wh = normalize(wo + wi * eta);
+        if (wh.z < 0) wh = -wh;
+        if (dot(wo, wh) * dot(wi, wh) > 0) return black;
+        const float F = fr_dielectric(dot(wo, wh), 1.f, b.eta);
+        const float sqrtDenom = dot(wo, wh) + eta * dot(wi, wh);
+        const float factor = 1 / eta;
+        const float v = fabsf(tr_D(ax, ay, wh) * tr_G(ax, ay, wo, wi) * eta * eta * absdot(wi, wh) * absdot(wo, wh) *
+                              factor * factor / (cosI * cosO * sqrtDenom * sqrtDenom));
+        return lobe_term(2, 1.f - F, v);
+    }
+    return black;
+}
+// hb_lobes_f's lobe selection, as terms
+template <int kFt>
+__device__ __forceinline__ HbTerms hb_terms_f(const Bsdf& b, V3 wo, V3 wi, bool reflect) {
+    HbTerms T;
+    T.n = 0;
+    T.generic = Ft<kFt>::micro && (b.m->kind == PT_MAT_METAL || b.m->kind == PT_MAT_PLASTIC);
+    auto sel = [&](int k) {
+        const int t = lobe_type(k);
+        return lobe_matches(k, kBxAll) && ((reflect && (t & kBxR)) || (!reflect && (t & kBxT)));
+    };
+    // at most two lobes; T.t[] is written at constant indices (no private array)
+    const bool s0 = b.n > 0 && sel(b.lk0), s1 = Ft<kFt>::max_lobes > 1 && b.n > 1 && sel(b.lk1);
+    if (s0) T.t[0] = lobe_f_term<kFt>(b, b.lk0, wo, wi);
+    if (s1) {
+        const LobeTerm t1 = lobe_f_term<kFt>(b, b.lk1, wo, wi);
+        if (s0) T.t[1] = t1;
+        else T.t[0] = t1;
+    }
+    T.n = (s0 ? 1 : 0) + (s1 ? 1 : 0);
+    return T;
+}
+// the value lobe_sample returned for a sampled specular lobe (local wo, wi;
+// `type` = the sampled BxDFType), as one term
+template <int kFt>
+__device__ __forceinline__ HbTerms hb_terms_spec(const Bsdf& b, int type, V3 wo, V3 wi) {
+    HbTerms T;
+    T.n = 1;
+    T.generic = false;
+    const int k = (lobe_type(b.lk0) & kBxSpecular) ? b.lk0 : b.lk1;
+    const float az = fabsf(wi.z);
+    const bool entering = wo.z > 0;
+    const float etaI = entering ? 1.f : b.eta, etaT = entering ? b.eta : 1.f;
+    const float ratio = (etaI * etaI) / (etaT * etaT);
+    if (k == kLbSpecRefl) T.t[0] = lobe_term(1, 1.f, 1.f, 1.f, az);
+    else if (k == kLbSpecReflD) T.t[0] = lobe_term(1, fr_dielectric(wi.z, 1.f, b.eta), 1.f, 1.f, az);
+    else if (k == kLbSpecTrans) T.t[0] = lobe_term(2, 1.f - fr_dielectric(wi.z, 1.f, b.eta), ratio, 1.f, az);
+    else {  // FresnelSpecular
+        const float F = fr_dielectric(wo.z, 1.f, b.eta);
+        T.t[0] = (type & kBxT) ? lobe_term(2, 1 - F, ratio, 1.f, az) : lobe_term(1, F, 1.f, 1.f, az);
+    }
+    return T;
+}
+// the terms at the chunk the BSDF currently holds, summed as BSDF::f does
+__device__ __forceinline__ S3 hb_eval(const HbTerms& T, const Bsdf& b) {
+    S3 f = s3(0.f);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (i >= T.n) break;
+        const LobeTerm& t = T.t[i];
+        if (t.src < 0) { f = f + s3(0.f); continue; }
+        const S3 X = clamp0(t.src == 0 ? b.rkd : (t.src == 1 ? b.rkr : b.rkt));
+        f = f + (((X * t.a) * t.b) * t.c) / t.d;
+    }
+    return f;
+}
+
 // BSDF::f over all 60 bins: the shading-frame change and the reflect test
 // once, the lobe values per 3-bin chunk; out(k, f) receives chunk k.
-template <typename Out>
-__device__ __forceinline__ void hb_f_all(const DevHero& h, HeroBsdf* hb, V3 woW, V3 wiW, Out out) {
-    const Bsdf& b = hb->b;
+// bsdf_f(b, woW, wiW, kBxAll) as terms: its frame change, wo.z == 0 test
+// (black: no terms) and lobe selection
+template <int kFt>
+__device__ __forceinline__ HbTerms hb_terms_world(const Bsdf& b, V3 woW, V3 wiW) {
     const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
-    const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    HbTerms T = hb_terms_f<kFt>(b, wo, wi, dot(wiW, b.ng) * dot(woW, b.ng) > 0);
+    if (wo.z == 0) T.n = 0;
+    return T;
+}
+// one bin of bsdf_f(b, woW, wiW) for the terms of those directions
+template <int kFt>
+__device__ __forceinline__ float hb_f1_t(const DevHero& h, HeroBsdf* hb, const HbTerms& T, V3 woW, V3 wiW, int bin) {
+    hb_chunk(h, hb, bin / 3);
+    return (T.generic ? bsdf_f<kFt>(hb->b, woW, wiW, kBxAll) : hb_eval(T, hb->b)).c[bin % 3];
+}
+template <int kFt, typename Out>
+__device__ __forceinline__ void hb_f_all(const DevHero& h, HeroBsdf* hb, const HbTerms& T, V3 woW, V3 wiW, Out out) {
+    const Bsdf& b = hb->b;
+    #pragma unroll 1
     for (int i0 = 0; i0 < kNS; i0 += kG) {  // out(i0, f) receives bins i0 .. i0 + kG - 1
         float f[kG];
         HbGroup g;
@@ -185,7 +299,7 @@ __device__ __forceinline__ void hb_f_all(const DevHero& h, HeroBsdf* hb, V3 woW,
 #pragma unroll
         for (int c = 0; c < kG / 3; ++c) {
             hb_chunk_g(hb, g, c);
-            const S3 v = wo.z == 0 ? s3(0.f) : hb_lobes_f(b, wo, wi, reflect);
+            const S3 v = T.generic ? bsdf_f<kFt>(b, woW, wiW, kBxAll) : hb_eval(T, b);
             f[3 * c] = v.c[0]; f[3 * c + 1] = v.c[1]; f[3 * c + 2] = v.c[2];
         }
         out(i0, f);
@@ -304,8 +418,9 @@ __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPa
 // first the pending light sample of the previous vertex (added if its shadow
 // ray came back unoccluded), then the hit of the continuation ray.  Emits the
 // shadow ray of SampleEmitterHero and the next continuation ray.
+template <int kFt>
 __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, const DevPaths& ps, const DevHeroPaths& hp,
-                          uint32_t slot, uint32_t* rays, uint32_t* nrays, bool* overflow) {
+                          uint32_t slot, uint32_t* rays, uint32_t* nrays, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     uint32_t st = ps.st[slot];
     float* Lg = hp.L + slot;
@@ -314,33 +429,59 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     float* H = hp.hs + slot;
     uint32_t hf = __float_as_uint(H[kHsFlags * N]);
     *nrays = 0;
+    // algorithmic path-state bytes: each 60-bin array (L, nee, beta) counted
+    // once per direction it is touched in this step (tch bits), plus the
+    // scalar fields and queue entries
+    uint32_t tch = 0, sb = 4 + 4 + 4 + 4 + 4;  // queue entry; st and H flags read and written
+    auto count = [&]() { *ab += sb + 4 * kNS * (uint32_t)__builtin_popcount(tch); };
     if (st & kStNee) {
+        if (hf & kHfPend) sb += 4;  // hitA
         if ((hf & kHfPend) && ps.hitA[slot] == 0)
+            #pragma unroll 1
             for (int i0 = 0; i0 < kNS; i0 += kG) {
                 float l[kG], x[kG];
-                gload(Lg, N, i0, l);
-                gload(Ng, N, i0, x);
+                tch |= 1u, gload(Lg, N, i0, l);
+                tch |= 2u, gload(Ng, N, i0, x);
 #pragma unroll
                 for (int j = 0; j < kG; ++j) l[j] += x[j];
-                gstore(Lg, N, i0, l);
+                tch |= 8u, gstore(Lg, N, i0, l);
             }
         st &= ~kStNee;
         hf &= ~kHfPend;
     }
     // the finished sample's radiance, slot-major for the film gather
     auto finish = [&]() {
-        float* o = h.out60 + (size_t)slot * kNS;
+        // 240 B per slot as 15 float4 stores; y = spectrum.h:407-413 with the
+        // bins summed in order, NaN test of hero.cpp:118-140 folded in
+        float4* o = reinterpret_cast<float4*>(h.out60 + (size_t)slot * kNS);
+        float yy = 0.f;
+        bool nan = false;
+        #pragma unroll 1
         for (int i0 = 0; i0 < kNS; i0 += kG) {
             float l[kG];
-            gload(Lg, N, i0, l);
+            tch |= 1u, gload(Lg, N, i0, l);
 #pragma unroll
-            for (int j = 0; j < kG; ++j) o[i0 + j] = l[j];
+            for (int j = 0; j < kG; ++j) {
+                yy += h.XYZ[kNS + i0 + j] * l[j];
+                nan |= __builtin_isnan(l[j]);
+            }
+            if constexpr (kG % 4 == 0) {
+#pragma unroll
+                for (int j = 0; j < kG; j += 4) o[(i0 + j) / 4] = make_float4(l[j], l[j + 1], l[j + 2], l[j + 3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < kG; ++j) h.out60[(size_t)slot * kNS + i0 + j] = l[j];
+            }
         }
+        const float yv = yy * (float)(700 - 400) / (float)(106.856895f * kNS);
+        h.out_y[slot] = nan ? -__builtin_inff() : yv;
+        sb += 4 * kNS + 4;
     };
     if (!(st & kStCont)) {
         H[kHsFlags * N] = __uint_as_float(hf);
         ps.st[slot] = st;
         finish();
+        count();
         return;
     }
     st &= ~kStCont;
@@ -358,21 +499,22 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     bool isWvlDependent = (hf & kHfWvlDep) != 0;
     const bool isLastSpecular = (hf & kHfLastSpec) != 0;
     Ray ray = load_ray6(ps.ray, N, slot, kInf);
+    sb += 4 + 56 + 24 + 4;  // hidx, H wavelengths / pdfs / etaScale / bsdfPdf, ray, hit
     const V3 rayO = ray.o;
     const int hpr = ps.hit[slot];
     SurfHit si;
-    const bool found = hpr >= 0 && surface_at<true>(sc, hpr, ray, &si);
-    float tmp[kNS];  // infinite lights' FromRGB(Illuminant) radiance
+    const bool found = hpr >= 0 && surface_at<Ft<kFt>::sph>(sc, hpr, ray, &si);
     // Lo += beta * Le, weighted (hero_path.cpp:84-104, hero_path_mis.cpp:120-166)
     auto add_emitted = [&](auto Le, float emPdf) {
         const float sw = pathWvlPdf[0] + pathWvlPdf[1] + pathWvlPdf[2] + pathWvlPdf[3];
         const float s = (pathWvlPdf[0] + prev[0] * emPdf) + (pathWvlPdf[1] + prev[1] * emPdf) +
                         (pathWvlPdf[2] + prev[2] * emPdf) + (pathWvlPdf[3] + prev[3] * emPdf);
         const float mwc = bsdfPdf / (bsdfPdf + emPdf);
+        #pragma unroll 1
         for (int i0 = 0; i0 < kNS; i0 += kG) {
             float l[kG], bv[kG];
-            gload(Lg, N, i0, l);
-            gload(Bg, N, i0, bv);
+            tch |= 1u, gload(Lg, N, i0, l);
+            tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
             for (int j = 0; j < kG; ++j) {
                 const int i = i0 + j;
@@ -383,22 +525,24 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                 else
                     l[j] += (bv[j] * Le(i)) * (isWvlDependent ? 1.0f / (wvl_pdf(h, wvlIdx, i) * s) : mwc);
             }
-            gstore(Lg, N, i0, l);
+            tch |= 8u, gstore(Lg, N, i0, l);
         }
     };
     bool cont = false;
     if (!found) {
-        for (int li = 0; li < sc.n_lights; ++li) {
+        for (int li = 0; Ft<kFt>::inf && li < sc.n_lights; ++li) {
             const DevLight& l = sc.lights[li];
             if (l.kind != PT_LIGHT_INFINITE) continue;
-            s60_from_rgb_illum(h, inf_Le(l, ray.d), tmp);  // Spectrum(Lmap->Lookup, Illuminant)
-            if (s60_black(tmp)) continue;
+            const RgbIllum ri = rgb_illum(inf_Le(l, ray.d));  // Spectrum(Lmap->Lookup, Illuminant)
+            bool black = true;
+            for (int i = 0; i < kNS; ++i) black &= rgb_illum_bin(h, ri, i) == 0.f;
+            if (black) continue;
             const float emPdf = (h.mis && bounces > 0 && !isLastSpecular) ? inf_pdf_li(l, ray.d) : 0.f;
-            add_emitted([&](int i) { return tmp[i]; }, emPdf);
+            add_emitted([&](int i) { return rgb_illum_bin(h, ri, i); }, emPdf);
         }
     } else {
         int mat, light;
-        prim_info<true>(sc, hpr, &mat, &light);
+        prim_info<Ft<kFt>::sph>(sc, hpr, &mat, &light);
         if (light >= 0) {
             const DevLight& l = sc.lights[PT_IDX(light, sc.n_lights)];
             const bool vis = l.two_sided || dot(si.n, -ray.d) > 0;  // DiffuseAreaLight::L
@@ -421,6 +565,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         if (bounces >= sc.max_depth) {
         } else if (M.kind == PT_MAT_NONE) {  // bounces-- ; continue
             store_ray6(ps.ray, N, slot, Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf});
+            sb += 24;
             rays[(*nrays)++] = slot << 2 | kRayCont;
             cont = true;
         } else {
@@ -433,22 +578,23 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                 for (int i = 0; i < 4; ++i) etas[i] = cauchyB + cauchyC / (wvls[i] * wvls[i]);
             }
             HeroBsdf hb0;
-            hb_make(sc, h, mat, si, etas[0], &hb0);
+            hb_make<kFt>(sc, h, mat, si, etas[0], &hb0);
             const bool isectWvlDep = disp && hb0.b.n > 0;
             // f and pdf of the i-th wavelength's BSDF at one bin
-            auto f1_pdf = [&](bool perWvl, int i, V3 wo, V3 wi, int bin, float* pdf) {
+            // f and pdf of the i-th wavelength's BSDF at one bin; T0 / pdf0: hb0's
+            // terms and pdf at (wo, wi)
+            auto f1_pdf = [&](bool perWvl, int i, const HbTerms& T0, float pdf0, V3 wo, V3 wi, int bin, float* pdf) {
                 if (!perWvl || i == 0) {
-                    const float f = hb_f1(h, &hb0, wo, wi, bin);
-                    *pdf = bsdf_pdf<kFtAll>(hb0.b, wo, wi, kBxAll);
-                    return f;
+                    *pdf = pdf0;
+                    return hb_f1_t<kFt>(h, &hb0, T0, wo, wi, bin);
                 }
                 HeroBsdf hbi;
-                hb_make(sc, h, mat, si, etas[i], &hbi);
-                const float f = hb_f1(h, &hbi, wo, wi, bin);
-                *pdf = bsdf_pdf<kFtAll>(hbi.b, wo, wi, kBxAll);
+                hb_make<kFt>(sc, h, mat, si, etas[i], &hbi);
+                const float f = hb_f1<kFt>(h, &hbi, wo, wi, bin);
+                *pdf = bsdf_pdf<kFt>(hbi.b, wo, wi, kBxAll);
                 return f;
             };
-            if (h.mis && bsdf_num<kFtAll>(hb0.b, kBxNonSpecular) > 0 && sc.n_lights > 0) {
+            if (h.mis && bsdf_num<kFt>(hb0.b, kBxNonSpecular) > 0 && sc.n_lights > 0) {
                 // SampleEmitterHero (hero_path_mis.cpp:78-108); the shadow ray is
                 // traced by the next k_trace and the term added by the next step
                 const float* d = hero_dist(h, si.p);
@@ -461,7 +607,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                     float epdf = 0;
                     V3 wi = v3(0, 0, 0), sp, sn, spe;
                     const DevLight& l = sc.lights[PT_IDX(li, sc.n_lights)];
-                    const S3 Lrgb = area_sample_li<kFtAll>(sc, l, si, u0, u1, &wi, &epdf, &sp, &sn, &spe);
+                    const S3 Lrgb = area_sample_li<kFt>(sc, l, si, u0, u1, &wi, &epdf, &sp, &sn, &spe);
                     if (epdf != 0.f) {
                         const V3 origin = offset_ray_origin(si.p, si.perr, si.n, sp - si.p);
                         const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
@@ -470,45 +616,49 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
                         a[3 * N + slot] = dd.x; a[4 * N + slot] = dd.y; a[5 * N + slot] = dd.z;
                         a[6 * N + slot] = 1 - kShadowEps;
+                        sb += 28;
                         rays[(*nrays)++] = slot << 2 | kRayShadow;
                         st |= kStNee;
                         // the term as if unoccluded
                         emPdf = emPdf * epdf;
                         const bool inf = l.kind == PT_LIGHT_INFINITE;
                         const bool vis = inf || l.two_sided || dot(sn, -wi) > 0;
-                        if (inf) s60_from_rgb_illum(h, Lrgb, tmp);
+                        const RgbIllum ri = rgb_illum(Lrgb);
                         const float* Lrow = h.light_s60 + (size_t)li * kNS;
-                        auto Li = [&](int i) { return (inf ? tmp[i] : (vis ? Lrow[i] : 0.f)) / emPdf; };
+                        auto Li = [&](int i) { return (inf ? rgb_illum_bin(h, ri, i) : (vis ? Lrow[i] : 0.f)) / emPdf; };
                         bool haveLi = false;
                         for (int i = 0; i < kNS; ++i) haveLi |= Li(i) != 0.f;
                         if (haveLi && emPdf > 0.f) {
                             const V3 wo = si.wo;
                             const float cosv = absdot(wi, si.sn);
                             const bool depN = isWvlDependent || isectWvlDep;
-                            const float mwn = depN ? 0.f : emPdf / (emPdf + bsdf_pdf<kFtAll>(hb0.b, wo, wi, kBxAll));
+                            const HbTerms Tn = hb_terms_world<kFt>(hb0.b, wo, wi);
+                            const float pdfn = bsdf_pdf<kFt>(hb0.b, wo, wi, kBxAll);
+                            const float mwn = depN ? 0.f : emPdf / (emPdf + pdfn);
                             bool fnb = false;  // !IsBlack(f); the term itself when no bin is wavelength-dependent
-                            hb_f_all(h, &hb0, wo, wi, [&](int i0, const float* f) {
+                            hb_f_all<kFt>(h, &hb0, Tn, wo, wi, [&](int i0, const float* f) {
 #pragma unroll
                                 for (int j = 0; j < kG; ++j) fnb |= f[j] != 0.f;
                                 if (!depN) {
                                     float bv[kG], nv[kG];
-                                    gload(Bg, N, i0, bv);
+                                    tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
                                     for (int j = 0; j < kG; ++j) nv[j] = ((bv[j] * Li(i0 + j)) * (f[j] * cosv)) * mwn;
-                                    gstore(Ng, N, i0, nv);
+                                    tch |= 16u, gstore(Ng, N, i0, nv);
                                 }
                             });
                             if (fnb) {
                                 if (depN) {
                                     float fv[4], bp[4];
-                                    for (int i = 0; i < 4; ++i) fv[i] = f1_pdf(isectWvlDep, i, wo, wi, wvlIdx[i], &bp[i]);
+                                    for (int i = 0; i < 4; ++i) fv[i] = f1_pdf(isectWvlDep, i, Tn, pdfn, wo, wi, wvlIdx[i], &bp[i]);
                                     const float s = (pathWvlPdf[0] * emPdf + pathWvlPdf[0] * bp[0]) +
                                                     (pathWvlPdf[1] * emPdf + pathWvlPdf[1] * bp[1]) +
                                                     (pathWvlPdf[2] * emPdf + pathWvlPdf[2] * bp[2]) +
                                                     (pathWvlPdf[3] * emPdf + pathWvlPdf[3] * bp[3]);
+                                    #pragma unroll 1
                                     for (int i0 = 0; i0 < kNS; i0 += kG) {
                                         float bv[kG], nv[kG];
-                                        gload(Bg, N, i0, bv);
+                                        tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
                                         for (int j = 0; j < kG; ++j) {
                                             const int b = i0 + j;
@@ -518,7 +668,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                             const float mw = emPdf / (wvl_pdf(h, wvlIdx, b) * s);
                                             nv[j] = ((bv[j] * Li(b)) * (f * cosv)) * mw;
                                         }
-                                        gstore(Ng, N, i0, nv);
+                                        tch |= 16u, gstore(Ng, N, i0, nv);
                                     }
                                 }
                                 hf |= kHfPend;
@@ -536,20 +686,23 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
             bool fnb = false, curWvlDep = false, dep = false;
             float keep0 = 0.f;  // f[wvlIdx[0]]
             // the direction, pdf and lobe type do not depend on the reflectances:
-            // sample at chunk 0, then only the values of the other chunks (a
-            // specular lobe is cheap to re-run; a non-specular one is BSDF::f's
-            // lobe sum at the sampled local direction, as in BSDF::Sample_f)
+            // sample at chunk 0, then only the values of the other chunks (the
+            // sampled specular lobe's value, or BSDF::f's lobe sum at the sampled
+            // local direction as in BSDF::Sample_f), from the factored terms
             V3 woL = v3(0, 0, 0), wiL = v3(0, 0, 0);
             bool reflectS = false, specS = false;
             {
                 hb_chunk(h, &hb0, 0);
-                const S3 v0 = bsdf_sample<kFtAll>(hb0.b, wo, &wi, u0, u1, &bsdfPdf, kBxAll, &flags, &wiL);
+                const S3 v0 = bsdf_sample<kFt>(hb0.b, wo, &wi, u0, u1, &bsdfPdf, kBxAll, &flags, &wiL);
                 curWvlDep = isectWvlDep && (flags & kBxT);
                 dep = isWvlDependent || curWvlDep;
                 specS = (flags & kBxSpecular) != 0;
                 woL = w2l(hb0.b, wo);
                 reflectS = dot(wi, hb0.b.ng) * dot(wo, hb0.b.ng) > 0;
+                const HbTerms T = specS ? hb_terms_spec<kFt>(hb0.b, flags, woL, wiL)
+                                        : hb_terms_f<kFt>(hb0.b, woL, wiL, reflectS);
                 const float cosv = absdot(wi, si.sn);
+                #pragma unroll 1
                 for (int i0 = 0; bsdfPdf != 0.f && i0 < kNS; i0 += kG) {  // pdf 0: every chunk returns 0
                     float f[kG];
                     HbGroup g;
@@ -560,14 +713,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         S3 v = v0;
                         if (k > 0) {
                             hb_chunk_g(&hb0, g, c);
-                            if (specS) {
-                                int fl2 = 0;
-                                float pdf2 = 0;
-                                V3 wi2;
-                                v = bsdf_sample<kFtAll>(hb0.b, wo, &wi2, u0, u1, &pdf2, kBxAll, &fl2);
-                            } else {
-                                v = hb_lobes_f(hb0.b, woL, wiL, reflectS);
-                            }
+                            v = T.generic ? hb_lobes_f<kFt>(hb0.b, woL, wiL, reflectS) : hb_eval(T, hb0.b);
                         }
                         f[3 * c] = v.c[0]; f[3 * c + 1] = v.c[1]; f[3 * c + 2] = v.c[2];
                     }
@@ -578,10 +724,10 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                     }
                     if (!dep) {  // beta *= f |cos| / pdf (unused if f is black)
                         float bv[kG];
-                        gload(Bg, N, i0, bv);
+                        tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
                         for (int j = 0; j < kG; ++j) bv[j] *= (f[j] * cosv) / bsdfPdf;
-                        gstore(Bg, N, i0, bv);
+                        tch |= 32u, gstore(Bg, N, i0, bv);
                     }
                 }
             }
@@ -592,14 +738,23 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                     float fv[4];
                     fv[0] = keep0;  // zeroAllBinsBut(wvlIdx[0])
                     pathWvlPdf[0] *= bsdfPdf;
+                    HbTerms Td;
+                    Td.n = 0;
+                    Td.generic = false;
+                    float pdfd = 0.f;
+                    if (!curWvlDep) {  // every wavelength takes hb0 at (wo, wi)
+                        Td = hb_terms_world<kFt>(hb0.b, wo, wi);
+                        pdfd = bsdf_pdf<kFt>(hb0.b, wo, wi, kBxAll);
+                    }
                     for (int i = 1; i < 4; ++i) {
                         float p;
-                        fv[i] = f1_pdf(curWvlDep, i, wo, wi, wvlIdx[i], &p);
+                        fv[i] = f1_pdf(curWvlDep, i, Td, pdfd, wo, wi, wvlIdx[i], &p);
                         pathWvlPdf[i] *= p;
                     }
+                    #pragma unroll 1
                     for (int i0 = 0; i0 < kNS; i0 += kG) {
                         float bv[kG];
-                        gload(Bg, N, i0, bv);
+                        tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
                         for (int j = 0; j < kG; ++j) {
                             const int b = i0 + j;
@@ -608,30 +763,31 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                 if (wvlIdx[i] == b) f += fv[i];
                             bv[j] *= f * cosv;
                         }
-                        gstore(Bg, N, i0, bv);
+                        tch |= 32u, gstore(Bg, N, i0, bv);
                     }
                 }
                 bool bnb = false;
-                for (int i = 0; i < kNS; ++i) bnb |= Bg[i * N] != 0.f;
+                for (int i = 0; i < kNS; ++i) bnb |= (tch |= 4u, Bg[i * N]) != 0.f;
                 if (bnb) {
                     ray = Ray{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     if ((flags & kBxSpecular) && (flags & kBxT)) {
                         const float eta = hb0.b.eta;
                         etaScale *= (dot(wo, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
                     }
-                    float mc = Bg[0] * etaScale;
-                    for (int i = 1; i < kNS; ++i) mc = smax(mc, Bg[i * N] * etaScale);
+                    float mc = Bg[0] * etaScale;  // beta read above
+                    for (int i = 1; i < kNS; ++i) mc = smax(mc, (tch |= 4u, Bg[i * N]) * etaScale);
                     bool alive = true;
                     if (mc < sc.rr_threshold && bounces > 3) {
                         const float q = smax(0.05f, 1 - mc);
                         if (dm.get1() < q) alive = false;
                         else
+                            #pragma unroll 1
                             for (int i0 = 0; i0 < kNS; i0 += kG) {
                                 float bv[kG];
-                                gload(Bg, N, i0, bv);
+                                tch |= 4u, gload(Bg, N, i0, bv);
 #pragma unroll
                                 for (int j = 0; j < kG; ++j) bv[j] /= 1 - q;
-                                gstore(Bg, N, i0, bv);
+                                tch |= 32u, gstore(Bg, N, i0, bv);
                             }
                     }
                     if (alive) {
@@ -639,6 +795,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         hf = (hf & ~(kHfWvlDep | kHfLastSpec)) | (isWvlDependent ? kHfWvlDep : 0u) |
                              ((flags & kBxSpecular) ? kHfLastSpec : 0u);
                         store_ray6(ps.ray, N, slot, ray);
+                        sb += 24 + 40;  // ray; H pdfs / etaScale / bsdfPdf
                         rays[(*nrays)++] = slot << 2 | kRayCont;
                         cont = true;
                         ++bounces;
@@ -660,8 +817,11 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     H[kHsFlags * N] = __uint_as_float(hf);
     ps.st[slot] = st;
     if (!(st & (kStCont | kStNee))) finish();
+    sb += 4 * (*nrays + ((st & (kStCont | kStNee)) ? 1u : 0u));  // ray / path queue entries written
+    count();
 }
 
+template <int kFt>
 __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHero& h, const DevPaths& ps,
                                                  const DevHeroPaths& hp, const uint32_t* __restrict__ pq,
                                                  const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
@@ -670,6 +830,7 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
     const uint32_t n = *pq_count;
     bool overflow = false;
     PT_WAVEQ(wq);
+    uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         uint32_t rays[3];
@@ -678,23 +839,25 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
         uint32_t slot = 0;
         if (i < n) {
             slot = pq[i];
-            hero_step(sc, h, ps, hp, slot, rays, &nrays, &overflow);
+            hero_step<kFt>(sc, h, ps, hp, slot, rays, &nrays, &overflow, &ab);
             keep = (ps.st[slot] & (kStCont | kStNee)) != 0;
         }
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
+    const unsigned long long abw = wave_sum_u64((unsigned long long)ab);
+    if (lane_id() == 0 && abw) atomicAdd(&stats->shade_bytes, abw);
 }
 
 // register-budget variants (PT_HERO_WAVES): compiler default, 2 or 4 waves per SIMD
 #define PT_HERO_SHADE(name, attr)                                                                                   \
-    __global__ __launch_bounds__(kShadeBlock) attr void name(                                                      \
+    template <int kFt> __global__ __launch_bounds__(kShadeBlock) attr void name(                                                      \
         DevScene sc, DevHero h, DevPaths ps, DevHeroPaths hp, const uint32_t* __restrict__ pq,                     \
         const uint32_t* __restrict__ pq_count, uint32_t* rq_out, uint32_t* rq_out_count, uint32_t* pq_out,        \
         uint32_t* pq_out_count, DevStats* stats) PT_HERO_BODY
 #ifdef PT_TU_HERO
-#define PT_HERO_BODY { shade_hero_batch(sc, h, ps, hp, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats); }
+#define PT_HERO_BODY { shade_hero_batch<kFt>(sc, h, ps, hp, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats); }
 #else
 #define PT_HERO_BODY ;
 #endif
@@ -751,11 +914,8 @@ __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmCo
                                 touch = !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
                                 if (touch) {
                                     // radiance sanitiser (hero.cpp:118-140) and maxSampleLuminance
-                                    const float* L = h.out60 + (size_t)slot * kNS;
-                                    bool nan = false;
-                                    for (int i = 0; i < kNS; ++i) nan |= __builtin_isnan(L[i]);
-                                    const float yv = s60_y(h, L);
-                                    if (nan || (double)yv < -1e-5 || __builtin_isinf(yv)) k = 0.f;
+                                    const float yv = h.out_y[slot];  // -inf: a NaN bin
+                                    if ((double)yv < -1e-5 || __builtin_isinf(yv)) k = 0.f;
                                     else if (yv > fc.max_lum) k = fc.max_lum / yv;
                                     else k = 1.f;
                                     const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);

@@ -171,7 +171,7 @@ struct Work {
     DBuf<DevStats> stats;
     DBuf<int> dli;                 // DirectLighting state (kDl*)
     DBuf<float> dlf, dlframe;
-    DBuf<float> h_out60, h_L60, h_beta60, h_nee60, h_hs;  // hero integrators: 60-bin state per slot
+    DBuf<float> h_out60, h_outy, h_L60, h_beta60, h_nee60, h_hs;  // hero integrators: 60-bin state per slot
     size_t cap = 0, hero_cap = 0;
     int dl_frames = 0;             // > 0: DirectLighting buffers with this many frames per slot
     hipStream_t stream = nullptr;  // this pipeline's stream (render_tiles)
@@ -192,6 +192,7 @@ struct Work {
         }
         if (hero_slots > 0 && (size_t)hero_slots > hero_cap) {
             h_out60.alloc((size_t)hero_slots * kNSpec);
+            h_outy.alloc((size_t)hero_slots);
             h_L60.alloc((size_t)hero_slots * kNSpec);
             h_beta60.alloc((size_t)hero_slots * kNSpec);
             h_nee60.alloc((size_t)hero_slots * kNSpec);
@@ -260,7 +261,7 @@ struct pt_scene {
     size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (8 M for the 60-bin hero state)
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
-    int hero_waves = 4;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4)
+    int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
     int shade_variant = 0;       // 0: compiler register budget (no scratch), 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
@@ -324,6 +325,27 @@ static ShadeKernel shade_kernel(int variant, int features) {
         case kFtSphere: return shade_kernel_ft<kFtSphere>(variant);
         case kFtInfinite | kFtSphere: return shade_kernel_ft<kFtInfinite | kFtSphere>(variant);
         default: return shade_kernel_ft<kFtAll>(variant);
+    }
+}
+
+using HeroKernel = void (*)(DevScene, DevHero, DevPaths, DevHeroPaths, const uint32_t*, const uint32_t*, uint32_t*,
+                           uint32_t*, uint32_t*, uint32_t*, DevStats*);
+template <int kFt>
+static HeroKernel hero_kernel_ft(int waves) {
+    return waves == 1 ? k_shade_hero<kFt> : (waves == 2 ? k_shade_hero_w2<kFt> : k_shade_hero_w4<kFt>);
+}
+// instantiated (tu_hero.hip): matte-only, smooth specular, + infinite light, no spheres, everything
+static HeroKernel hero_kernel(int waves, int features) {
+    switch (features & kFtAll) {
+        case 0: return hero_kernel_ft<0>(waves);
+        case kFtSpecular: return hero_kernel_ft<kFtSpecular>(waves);
+        case kFtInfinite:
+        case kFtSpecular | kFtInfinite: return hero_kernel_ft<kFtSpecular | kFtInfinite>(waves);
+        case kFtMicro:
+        case kFtMicro | kFtSpecular:
+        case kFtMicro | kFtInfinite:
+        case kFtMicro | kFtSpecular | kFtInfinite: return hero_kernel_ft<kFtMicro | kFtSpecular | kFtInfinite>(waves);
+        default: return hero_kernel_ft<kFtAll>(waves);
     }
 }
 
@@ -1118,6 +1140,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         DevHero hh = s->hh;
         if (s->hero) {
             hh.out60 = w.h_out60.p;
+            hh.out_y = w.h_outy.p;
             hps = DevHeroPaths{w.h_beta60.p, w.h_L60.p, w.h_nee60.p, w.h_hs.p};
         }
         std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
@@ -1189,7 +1212,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 auto es = tev_new(true);
                 HIPCHK(hipEventRecord(es.first, st));
                 if (s->hero) {
-                    hipLaunchKernelGGL(s->hero_waves == 1 ? k_shade_hero : (s->hero_waves == 2 ? k_shade_hero_w2 : k_shade_hero_w4),
+                    hipLaunchKernelGGL(hero_kernel(s->hero_waves, s->features),
                                        sg, dim3(kShadeBlock), 0, st, s->dev, hh, ps, hps, pq_in, counts + 1, rq_out,
                                        counts + 2, pq_out, counts + 3, w.stats.p);
                 } else {

@@ -185,13 +185,20 @@ def test_spectral_furnace_known_answer(tmp_path, integrator):
     assert np.allclose(img.reshape(-1, 3).mean(0), expect, rtol=0.02), (img.reshape(-1, 3).mean(0), expect)
 
 
-def _c3_variant(tmp_path, integrator, res=40, spp=8):
+def _c3_variant(tmp_path, integrator, res=40, spp=8, smooth=False, no_infinite=False):
+    """smooth: the microfacet glass block made specular; no_infinite: the
+    environment light dropped -- the hero kernel then runs its
+    specular(+infinite) feature instantiation instead of the full one."""
     txt = open(os.path.join(SCENES, "cornell_dielectric.pbrt")).read()
+    if smooth:
+        txt = re.sub(r'"float [uv]roughness" \[ *[0-9.]+ *\]', "", txt)
+    if no_infinite:
+        txt = re.sub(r'LightSource "infinite"[^\n]*\n(\s*"spectrum [^\n]*\n)*', "", txt)
     txt = txt.replace('Integrator "path" "integer maxdepth" [5]', 'Integrator "%s"' % integrator)
     txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [%d]' % res, txt)
     txt = re.sub(r'"integer yresolution" \[\d+\]', '"integer yresolution" [%d]' % res, txt)
     txt = re.sub(r'"integer pixelsamples" \[\d+\]', '"integer pixelsamples" [%d]' % spp, txt)
-    p = tmp_path / f"c3_{integrator}.pbrt"
+    p = tmp_path / f"c3_{integrator}_{int(smooth)}{int(no_infinite)}.pbrt"
     p.write_text(txt)
     return str(p)
 
@@ -207,6 +214,25 @@ def test_hero_cornell_dielectric_matches_oracle(tmp_path, integrator):
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     got, gst = sc.render()
     print(f"{integrator}: mean={ref.mean():.5g} max|d|={np.abs(got - ref).max():.3g}")
+    assert ref.mean() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integrator", ["hero_path", "hero_path_mis"])
+@pytest.mark.parametrize("no_infinite", [False, True])
+def test_hero_cornell_dielectric_smooth_matches_oracle(tmp_path, integrator, no_infinite):
+    """Both glass blocks specular (and optionally no environment light): the
+    scene needs no microfacet lobes, so the device runs the smaller feature
+    instantiations of the hero kernel (render.hip hero_kernel).  Bit-exact."""
+    hs = ptgpu.HostScene(_c3_variant(tmp_path, integrator, smooth=True, no_infinite=no_infinite))
+    MATTE, DISPERSIVE = 1, 4  # include/pt.h PT_MAT_*
+    assert all(m.kind in (MATTE, DISPERSIVE) and (m.kind != DISPERSIVE or m.specular) for m in hs.materials())
+    sc = ptgpu.Scene(hs)
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    got, gst = sc.render()
     assert ref.mean() > 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
