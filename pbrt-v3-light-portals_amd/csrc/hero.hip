@@ -32,13 +32,36 @@ constexpr int kNS = 60;
 #endif
 constexpr int kG = PT_HERO_G;  // 3, 6 or 12 (whole 3-bin chunks)
 static_assert(kNS % kG == 0 && kG % 3 == 0, "bin groups hold whole chunks");
+// Layout of the per-slot 60-bin state (DevHeroPaths): slot-major (AoS, 240 B
+// per slot: a lane's bin group is one contiguous run of 16-byte loads, whatever
+// the spread of the slots in the path queue) or bin-major (stride n).
+#ifndef PT_HERO_AOS
+#define PT_HERO_AOS 1
+#endif
+constexpr bool kAos = PT_HERO_AOS != 0;
+// g: the slot's bin 0; N: the bin stride (1 slot-major, n bin-major)
 __device__ __forceinline__ void gload(const float* g, uint32_t N, int i0, float* r) {
+    if constexpr (kAos && kG % 4 == 0) {
+        const float4* p = reinterpret_cast<const float4*>(g + i0);
 #pragma unroll
-    for (int j = 0; j < kG; ++j) r[j] = g[(uint32_t)(i0 + j) * N];
+        for (int q = 0; q < kG / 4; ++q) {
+            const float4 v = p[q];
+            r[4 * q] = v.x; r[4 * q + 1] = v.y; r[4 * q + 2] = v.z; r[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kG; ++j) r[j] = g[(uint32_t)(i0 + j) * N];
+    }
 }
 __device__ __forceinline__ void gstore(float* g, uint32_t N, int i0, const float* r) {
+    if constexpr (kAos && kG % 4 == 0) {
+        float4* p = reinterpret_cast<float4*>(g + i0);
 #pragma unroll
-    for (int j = 0; j < kG; ++j) g[(uint32_t)(i0 + j) * N] = r[j];
+        for (int q = 0; q < kG / 4; ++q) p[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kG; ++j) g[(uint32_t)(i0 + j) * N] = r[j];
+    }
 }
 
 struct DevHero {
@@ -335,14 +358,14 @@ __device__ __forceinline__ void light_L60(const DevHero& h, const DevLight& l, i
     for (int i = 0; i < kNS; ++i) out[i] = vis ? L[i] : 0.f;
 }
 
-// Per-slot state of a hero path on the wavefront (bin-major SoA, stride n):
-// the 60-bin throughput, radiance and pending light-sample contribution, and
-// the scalars of hero_path*.cpp's loop.
+// Per-slot state of a hero path on the wavefront (kAos: slot-major, else
+// bin-major with stride n): the 60-bin throughput, radiance and pending
+// light-sample contribution, and the scalars of hero_path*.cpp's loop.
 struct DevHeroPaths {
     float* beta;  // 60 n
     float* L;     // 60 n; copied to DevHero::out60 (slot-major, k_film_s60's layout) when the path ends
     float* nee;   // 60 n: SampleEmitterHero's term, added if its shadow ray is unoccluded
-    float* hs;    // kHs n
+    float* hs;    // kHsPad n
 };
 constexpr int kHsWvl = 0;       // 4: the hero wavelengths
 constexpr int kHsPath = 4;      // 4: pathWvlPdf
@@ -351,6 +374,14 @@ constexpr int kHsEtaScale = 12;
 constexpr int kHsBsdfPdf = 13;
 constexpr int kHsFlags = 14;    // kHf* (uint bits)
 constexpr int kHs = 15;
+constexpr int kHsPad = 16;  // scalars per slot when slot-major (64 B)
+// index of bin / scalar i of a slot
+__device__ __forceinline__ size_t hbin_at(uint32_t N, uint32_t slot, int i) {
+    return kAos ? (size_t)slot * kNS + i : (size_t)i * N + slot;
+}
+__device__ __forceinline__ size_t hs_at(uint32_t N, uint32_t slot, int i) {
+    return kAos ? (size_t)slot * kHsPad + i : (size_t)i * N + slot;
+}
 constexpr uint32_t kHfWvlDep = 1u, kHfLastSpec = 2u, kHfPend = 4u;
 
 
@@ -397,16 +428,16 @@ __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPa
             bin = bin < 0 ? 0 : (bin > kNS - 1 ? kNS - 1 : bin);
             const float minv = h.wcdf[bin], maxv = h.wcdf[bin + 1], diff = maxv - minv;
             const float alpha = (s - minv) / diff;
-            hp.hs[(kHsWvl + i) * N + slot] = (float)400 + (float)300 * ((alpha + (float)bin) / (float)kNS);
-            hp.hs[(kHsPath + i) * N + slot] = 1.f;
-            hp.hs[(kHsPrev + i) * N + slot] = 1.f;
+            hp.hs[hs_at(N, slot, kHsWvl + i)] = (float)400 + (float)300 * ((alpha + (float)bin) / (float)kNS);
+            hp.hs[hs_at(N, slot, kHsPath + i)] = 1.f;
+            hp.hs[hs_at(N, slot, kHsPrev + i)] = 1.f;
         }
-        hp.hs[kHsEtaScale * N + slot] = 1.f;
-        hp.hs[kHsBsdfPdf * N + slot] = 0.f;
-        hp.hs[kHsFlags * N + slot] = __uint_as_float(0u);
+        hp.hs[hs_at(N, slot, kHsEtaScale)] = 1.f;
+        hp.hs[hs_at(N, slot, kHsBsdfPdf)] = 0.f;
+        hp.hs[hs_at(N, slot, kHsFlags)] = __uint_as_float(0u);
         for (int b = 0; b < kNS; ++b) {
-            hp.beta[b * N + slot] = 1.f;
-            hp.L[b * N + slot] = 0.f;
+            hp.beta[hbin_at(N, slot, b)] = 1.f;
+            hp.L[hbin_at(N, slot, b)] = 0.f;
         }
     }
 }
@@ -423,11 +454,12 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                           uint32_t slot, uint32_t* rays, uint32_t* nrays, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     uint32_t st = ps.st[slot];
-    float* Lg = hp.L + slot;
-    float* Bg = hp.beta + slot;
-    float* Ng = hp.nee + slot;
-    float* H = hp.hs + slot;
-    uint32_t hf = __float_as_uint(H[kHsFlags * N]);
+    float* Lg = hp.L + hbin_at(N, slot, 0);
+    float* Bg = hp.beta + hbin_at(N, slot, 0);
+    float* Ng = hp.nee + hbin_at(N, slot, 0);
+    float* H = hp.hs + hs_at(N, slot, 0);
+    const uint32_t BS = kAos ? 1u : N;  // bin / scalar stride
+    uint32_t hf = __float_as_uint(H[kHsFlags * BS]);
     *nrays = 0;
     // algorithmic path-state bytes: each 60-bin array (L, nee, beta) counted
     // once per direction it is touched in this step (tch bits), plus the
@@ -440,11 +472,11 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
             #pragma unroll 1
             for (int i0 = 0; i0 < kNS; i0 += kG) {
                 float l[kG], x[kG];
-                tch |= 1u, gload(Lg, N, i0, l);
-                tch |= 2u, gload(Ng, N, i0, x);
+                tch |= 1u, gload(Lg, BS, i0, l);
+                tch |= 2u, gload(Ng, BS, i0, x);
 #pragma unroll
                 for (int j = 0; j < kG; ++j) l[j] += x[j];
-                tch |= 8u, gstore(Lg, N, i0, l);
+                tch |= 8u, gstore(Lg, BS, i0, l);
             }
         st &= ~kStNee;
         hf &= ~kHfPend;
@@ -459,7 +491,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         #pragma unroll 1
         for (int i0 = 0; i0 < kNS; i0 += kG) {
             float l[kG];
-            tch |= 1u, gload(Lg, N, i0, l);
+            tch |= 1u, gload(Lg, BS, i0, l);
 #pragma unroll
             for (int j = 0; j < kG; ++j) {
                 yy += h.XYZ[kNS + i0 + j] * l[j];
@@ -478,7 +510,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         sb += 4 * kNS + 4;
     };
     if (!(st & kStCont)) {
-        H[kHsFlags * N] = __uint_as_float(hf);
+        H[kHsFlags * BS] = __uint_as_float(hf);
         ps.st[slot] = st;
         finish();
         count();
@@ -490,12 +522,12 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     float wvls[4], pathWvlPdf[4], prev[4];
     int wvlIdx[4];
     for (int k = 0; k < 4; ++k) {
-        wvls[k] = H[(kHsWvl + k) * N];
+        wvls[k] = H[(kHsWvl + k) * BS];
         wvlIdx[k] = wvl_index(wvls[k]);
-        pathWvlPdf[k] = H[(kHsPath + k) * N];
-        prev[k] = H[(kHsPrev + k) * N];
+        pathWvlPdf[k] = H[(kHsPath + k) * BS];
+        prev[k] = H[(kHsPrev + k) * BS];
     }
-    float etaScale = H[kHsEtaScale * N], bsdfPdf = H[kHsBsdfPdf * N];
+    float etaScale = H[kHsEtaScale * BS], bsdfPdf = H[kHsBsdfPdf * BS];
     bool isWvlDependent = (hf & kHfWvlDep) != 0;
     const bool isLastSpecular = (hf & kHfLastSpec) != 0;
     Ray ray = load_ray6(ps.ray, N, slot, kInf);
@@ -513,8 +545,8 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         #pragma unroll 1
         for (int i0 = 0; i0 < kNS; i0 += kG) {
             float l[kG], bv[kG];
-            tch |= 1u, gload(Lg, N, i0, l);
-            tch |= 4u, gload(Bg, N, i0, bv);
+            tch |= 1u, gload(Lg, BS, i0, l);
+            tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
             for (int j = 0; j < kG; ++j) {
                 const int i = i0 + j;
@@ -525,7 +557,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                 else
                     l[j] += (bv[j] * Le(i)) * (isWvlDependent ? 1.0f / (wvl_pdf(h, wvlIdx, i) * s) : mwc);
             }
-            tch |= 8u, gstore(Lg, N, i0, l);
+            tch |= 8u, gstore(Lg, BS, i0, l);
         }
     };
     bool cont = false;
@@ -641,10 +673,10 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                 for (int j = 0; j < kG; ++j) fnb |= f[j] != 0.f;
                                 if (!depN) {
                                     float bv[kG], nv[kG];
-                                    tch |= 4u, gload(Bg, N, i0, bv);
+                                    tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
                                     for (int j = 0; j < kG; ++j) nv[j] = ((bv[j] * Li(i0 + j)) * (f[j] * cosv)) * mwn;
-                                    tch |= 16u, gstore(Ng, N, i0, nv);
+                                    tch |= 16u, gstore(Ng, BS, i0, nv);
                                 }
                             });
                             if (fnb) {
@@ -658,7 +690,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                     #pragma unroll 1
                                     for (int i0 = 0; i0 < kNS; i0 += kG) {
                                         float bv[kG], nv[kG];
-                                        tch |= 4u, gload(Bg, N, i0, bv);
+                                        tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
                                         for (int j = 0; j < kG; ++j) {
                                             const int b = i0 + j;
@@ -668,7 +700,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                             const float mw = emPdf / (wvl_pdf(h, wvlIdx, b) * s);
                                             nv[j] = ((bv[j] * Li(b)) * (f * cosv)) * mw;
                                         }
-                                        tch |= 16u, gstore(Ng, N, i0, nv);
+                                        tch |= 16u, gstore(Ng, BS, i0, nv);
                                     }
                                 }
                                 hf |= kHfPend;
@@ -724,10 +756,10 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                     }
                     if (!dep) {  // beta *= f |cos| / pdf (unused if f is black)
                         float bv[kG];
-                        tch |= 4u, gload(Bg, N, i0, bv);
+                        tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
                         for (int j = 0; j < kG; ++j) bv[j] *= (f[j] * cosv) / bsdfPdf;
-                        tch |= 32u, gstore(Bg, N, i0, bv);
+                        tch |= 32u, gstore(Bg, BS, i0, bv);
                     }
                 }
             }
@@ -754,7 +786,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                     #pragma unroll 1
                     for (int i0 = 0; i0 < kNS; i0 += kG) {
                         float bv[kG];
-                        tch |= 4u, gload(Bg, N, i0, bv);
+                        tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
                         for (int j = 0; j < kG; ++j) {
                             const int b = i0 + j;
@@ -763,11 +795,11 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                                 if (wvlIdx[i] == b) f += fv[i];
                             bv[j] *= f * cosv;
                         }
-                        tch |= 32u, gstore(Bg, N, i0, bv);
+                        tch |= 32u, gstore(Bg, BS, i0, bv);
                     }
                 }
                 bool bnb = false;
-                for (int i = 0; i < kNS; ++i) bnb |= (tch |= 4u, Bg[i * N]) != 0.f;
+                for (int i = 0; i < kNS; ++i) bnb |= (tch |= 4u, Bg[i * BS]) != 0.f;
                 if (bnb) {
                     ray = Ray{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     if ((flags & kBxSpecular) && (flags & kBxT)) {
@@ -775,7 +807,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         etaScale *= (dot(wo, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
                     }
                     float mc = Bg[0] * etaScale;  // beta read above
-                    for (int i = 1; i < kNS; ++i) mc = smax(mc, (tch |= 4u, Bg[i * N]) * etaScale);
+                    for (int i = 1; i < kNS; ++i) mc = smax(mc, (tch |= 4u, Bg[i * BS]) * etaScale);
                     bool alive = true;
                     if (mc < sc.rr_threshold && bounces > 3) {
                         const float q = smax(0.05f, 1 - mc);
@@ -784,10 +816,10 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                             #pragma unroll 1
                             for (int i0 = 0; i0 < kNS; i0 += kG) {
                                 float bv[kG];
-                                tch |= 4u, gload(Bg, N, i0, bv);
+                                tch |= 4u, gload(Bg, BS, i0, bv);
 #pragma unroll
                                 for (int j = 0; j < kG; ++j) bv[j] /= 1 - q;
-                                tch |= 32u, gstore(Bg, N, i0, bv);
+                                tch |= 32u, gstore(Bg, BS, i0, bv);
                             }
                     }
                     if (alive) {
@@ -800,11 +832,11 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         cont = true;
                         ++bounces;
                         for (int k = 0; k < 4; ++k) {
-                            H[(kHsPath + k) * N] = pathWvlPdf[k];
-                            H[(kHsPrev + k) * N] = prev[k];
+                            H[(kHsPath + k) * BS] = pathWvlPdf[k];
+                            H[(kHsPrev + k) * BS] = prev[k];
                         }
-                        H[kHsEtaScale * N] = etaScale;
-                        H[kHsBsdfPdf * N] = bsdfPdf;
+                        H[kHsEtaScale * BS] = etaScale;
+                        H[kHsBsdfPdf * BS] = bsdfPdf;
                     }
                 }
             }
@@ -814,7 +846,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
     st = (st & ~(kStDimMask | (0xffu << kStBounceShift))) | ((uint32_t)dm.dim & kStDimMask) |
          ((uint32_t)bounces << kStBounceShift);
-    H[kHsFlags * N] = __uint_as_float(hf);
+    H[kHsFlags * BS] = __uint_as_float(hf);
     ps.st[slot] = st;
     if (!(st & (kStCont | kStNee))) finish();
     sb += 4 * (*nrays + ((st & (kStCont | kStNee)) ? 1u : 0u));  // ray / path queue entries written

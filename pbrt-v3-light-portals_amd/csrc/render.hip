@@ -196,7 +196,7 @@ struct Work {
             h_L60.alloc((size_t)hero_slots * kNSpec);
             h_beta60.alloc((size_t)hero_slots * kNSpec);
             h_nee60.alloc((size_t)hero_slots * kNSpec);
-            h_hs.alloc((size_t)hero_slots * kHs);
+            h_hs.alloc((size_t)hero_slots * kHsPad);
             hero_cap = (size_t)hero_slots;
         }
         if (frames > 0 && (n > cap || frames != dl_frames)) {
