@@ -37,9 +37,9 @@ CONFIGS = {
     "c2": ("portal_cornell.pbrt", "portal Cornell (config 2)", "path maxdepth 5",
            "synthetic (scenes/portal_cornell.pbrt, procedural Cornell + portal; Halton sampler)"),
     "c3": ("cornell_dielectric.pbrt", "cornell dielectric (config 3)", "path maxdepth 5",
-           "reference scenes/cornell_dielectric.pbrt (spectral params reduced to RGB) with Integrator path, 1024 spp"),
+           "reference scenes/cornell_dielectric.pbrt (spectral params reduced to RGB) with Integrator path; file spp 1024"),
     "c3h": ("cornell_dielectric_hero.pbrt", "cornell dielectric as written (config 3)", "hero_path_mis",
-            "reference scenes/cornell_dielectric.pbrt as written (SampledSpectrum, Integrator hero_path_mis), 1024 spp"),
+            "reference scenes/cornell_dielectric.pbrt as written (SampledSpectrum, Integrator hero_path_mis; file spp 1024)"),
     "c4": ("portal_room.pbrt", "portal room (config 4)", "path maxdepth 8",
            "synthetic (scenes/portal_room.pbrt from scripts/make_portal_room.py: room + 4 portals + sky; Halton)"),
     "c5": ("killeroo_atrium.pbrt", "killeroo atrium 10M tris (config 5)", "path maxdepth 5",
@@ -291,7 +291,7 @@ def main():
             "scaling": shardmod.scaling(args.shard),
             "vs_baseline": None,
             "dtype": "f32",
-            "data": cdata,
+            "data": f"{cdata}; rendered at {spp} spp",
             "config": {"workload": workload, "resolution": [w, h],
                        "frame_spp": shardmod.frame_samples(spp, world, args.shard),
                        "parallelism": f"{args.shard} x{world}"},

@@ -240,6 +240,23 @@ def test_hero_cornell_dielectric_smooth_matches_oracle(tmp_path, integrator, no_
 
 
 @pytest.mark.gpu
+def test_hero_film_crop_and_batches_match_oracle(tmp_path):
+    """The 60-bin film (k_film_s60) under a crop window, an odd-sized film and
+    batches of a few FilmTiles (pixels on batch borders gather from several
+    launches) == the oracle, bit for bit."""
+    txt = open(_c3_variant(tmp_path, "hero_path_mis", res=40, spp=4)).read()
+    txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [53]', txt)
+    txt = txt.replace('Film "image"', 'Film "image" "float cropwindow" [0.13 0.91 0.08 0.77]')
+    p = tmp_path / "c3_crop.pbrt"
+    p.write_text(txt)
+    hs = ptgpu.HostScene(str(p))
+    ref, _ = pyoracle.render(hs.desc, nthreads=8)
+    got, _ = ptgpu.Scene(hs, batch_slots=16 * 16 * 4 * 3).render()  # 3 FilmTiles per batch
+    assert ref.mean() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("integrator", ["hero_path", "hero_path_mis"])
 def test_hero_furnace_matches_oracle(tmp_path, integrator):
     hs = ptgpu.HostScene(spectral_furnace(tmp_path, integrator, res=8, spp=16))
