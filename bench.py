@@ -172,7 +172,7 @@ def rooflines(agg: dict, workload: str, lds_scene: bool) -> dict:
         trf_s, src_s = pmc_traffic(workload, "k_shade")
         ks["k_shade"] = {"avg_launch_ms": round(avg_s, 4), "algorithmic_bytes_per_launch": round(alg_s, 1),
                          "algorithmic_GBs": round(alg_s / (avg_s * 1e-3) / 1e9, 1) if avg_s > 0 else 0.0,
-                         "data": "HBM (SoA path state)",
+                         "data": "HBM (path state)",
                          "hbm_traffic_per_launch": round(trf_s, 1) if trf_s is not None else None,
                          "hbm_GBs": round(trf_s / (avg_s * 1e-3) / 1e9, 1) if (trf_s is not None and avg_s > 0) else None,
                          "traffic_source": src_s, "total_ms": round(agg["shade_ms"], 2)}
