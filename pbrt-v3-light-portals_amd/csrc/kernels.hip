@@ -739,16 +739,18 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 // L += beta * Ld / lightPdf (integrator.cpp:121, path.cpp:122-127).
 // EstimateDirect's value from its traced rays (integrator.cpp:124-258,
 // portal_arealight.cpp:29-239): the Ld of the previous vertex's NEE.
+// fl / hA: the payload's flags and ray A's hit, when the caller has them
+// already (shade_batch prefetches them one path ahead).
 template <int kFt>
-__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
+__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
+                                        int hA) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
-    const uint32_t fl = __float_as_uint(nee[kNeeFlags * N + slot]);
     S3 Ld = s3(0.f);
     if (fl & kNfPortal) {
         if (fl & kNfA) {
             S3 Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
-            const int h = ps.hitA[slot];
+            const int h = hA;
             if (h >= 0) {
                 int lid;
                 Li = hit_Le<kFt>(sc, h, load_ray6(ps.rayA, N, slot, kInf), &lid);
@@ -758,7 +760,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
         }
         if (fl & kNfDivPortal) Ld = Ld / nee[kNeePortalPdf * N + slot];
     } else if (fl & kNfMis) {
-        if ((fl & kNfC1) && ps.hitA[slot] == 0)
+        if ((fl & kNfC1) && hA == 0)
             Ld = Ld + s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
         if (fl & kNfB) {
             const int h = ps.hitB[slot];
@@ -780,10 +782,15 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
     return Ld;
 }
 template <int kFt>
-__device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, S3* L) {
+__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
+    return nee_value<kFt>(sc, ps, slot, __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]), ps.hitA[slot]);
+}
+template <int kFt>
+__device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
+                                            int hA, S3* L) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
-    const S3 Ld = nee_value<kFt>(sc, ps, slot);
+    const S3 Ld = nee_value<kFt>(sc, ps, slot, fl, hA);
     const S3 bv = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
     *L = *L + bv * (Ld / nee[kNeeLpdf * N + slot]);
 }
@@ -969,24 +976,46 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
 
 // One path step.  Returns the rays to enqueue in rays[] and whether the path
 // stays alive.
-template <int kFt>
+// The fields every step reads first, loaded for the next path of a lane while
+// the current one is shaded (shade_batch): the kernel is bound by the latency
+// of its dependent loads, and these are the first two links of the chain.
+struct PathPre {
+    uint32_t st, hidx;
+    int hit, hitA;
+    uint32_t nfl;
+    S3 L, beta;
+    Ray ray;
+};
+__device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot, PathPre* p) {
+    const uint32_t N = (uint32_t)ps.n;
+    p->st = ps.st[slot];
+    p->hidx = ps.hidx[slot];
+    p->hit = ps.hit[slot];
+    p->hitA = ps.hitA[slot];
+    p->nfl = __float_as_uint(ps.nee[kNeeFlags * N + slot]);
+    p->L = load_s3(ps.L, N, slot);
+    p->beta = load_s3(ps.beta, N, slot);
+    p->ray = load_ray6(ps.ray, N, slot, kInf);
+}
+
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
 // k_shade roofline): the SoA fields the reference's Li loop carries from one
 // vertex to the next, plus the queue entries (scene tables are not counted).
-__device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
-                                           uint32_t* nrays, bool* keep, bool* overflow, uint32_t* ab) {
+template <int kFt>
+__device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, const PathPre& pre,
+                                           uint32_t* rays, uint32_t* nrays, bool* keep, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     *nrays = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
-    uint32_t st = ps.st[slot];
-    S3 L = load_s3(ps.L, N, slot);
+    uint32_t st = pre.st;
+    S3 L = pre.L;
     *ab += 4 + 4 + 12 + 12 + 4;  // queue entry, st + L read, L + st written
     if (st & kStNee) {
+        const uint32_t fl = pre.nfl;
         {   // bytes of the NEE payload resolve_nee reads (integrator.cpp:121, portal_arealight.cpp:29-239)
-            const uint32_t fl = __float_as_uint(ps.nee[kNeeFlags * N + slot]);
             uint32_t b = 4 + 12 + 4;  // flags, beta, light-selection pdf
             if (fl & kNfPortal) {
-                if (fl & kNfA) b += 12 + 4 + 12 + 4 + (ps.hitA[slot] >= 0 ? 24 : 0);
+                if (fl & kNfA) b += 12 + 4 + 12 + 4 + (pre.hitA >= 0 ? 24 : 0);
                 if (fl & kNfDivPortal) b += 4;
             } else if (fl & kNfMis) {
                 if (fl & kNfC1) b += 4 + 12;
@@ -994,16 +1023,16 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
             }
             *ab += b;
         }
-        resolve_nee<kFt>(sc, ps, slot, &L);
+        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, &L);
         st &= ~kStNee;
     }
     if (st & kStCont) {
         st &= ~kStCont;
         int bounces = (int)((st >> kStBounceShift) & 0xffu);
         const bool specular = (st & kStSpecular) != 0;
-        const Ray ray = load_ray6(ps.ray, N, slot, kInf);
-        const int hp = ps.hit[slot];
-        S3 beta = load_s3(ps.beta, N, slot);
+        const Ray ray = pre.ray;
+        const int hp = pre.hit;
+        S3 beta = pre.beta;
         *ab += 24 + 4 + 12;
         SurfHit si;
         bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &si);
@@ -1024,7 +1053,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 st |= kStCont;
                 rays[(*nrays)++] = slot << 2 | kRayCont;
             } else {
-                Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+                Dims dm{&sc, pre.hidx, (int)(st & kStDimMask), false};
                 *ab += 4;
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
@@ -1122,17 +1151,33 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     bool overflow = false;
     PT_WAVEQ(wq);
     uint32_t ab = 0;  // this lane's algorithmic path-state bytes
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    // software pipeline over the grid-stride iterations: the queue entry two
+    // paths ahead and the state of the next path are in flight while this
+    // path is shaded (slots in the queue are distinct, so no step writes what
+    // a prefetch read)
+    uint32_t base = blockIdx.x * blockDim.x;
+    uint32_t slot = 0, slot1 = 0;
+    PathPre pre{};
+    if (base + threadIdx.x < n) {
+        slot = pq[base + threadIdx.x];
+        path_prefetch(ps, slot, &pre);
+    }
+    if (base + stride + threadIdx.x < n) slot1 = pq[base + stride + threadIdx.x];
+    for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
+        PathPre nxt{};
+        uint32_t slot2 = 0;
+        if (i + stride < n) path_prefetch(ps, slot1, &nxt);
+        if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
         uint32_t rays[3];
         uint32_t nrays = 0;
         bool keep = false;
-        uint32_t slot = 0;
-        if (i < n) {
-            slot = pq[i];
-            shade_path<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow, &ab);
-        }
+        if (i < n) shade_path<kFt>(sc, ps, slot, pre, rays, &nrays, &keep, &overflow, &ab);
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+        slot = slot1;
+        slot1 = slot2;
+        pre = nxt;
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
