@@ -739,29 +739,46 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 // L += beta * Ld / lightPdf (integrator.cpp:121, path.cpp:122-127).
 // EstimateDirect's value from its traced rays (integrator.cpp:124-258,
 // portal_arealight.cpp:29-239): the Ld of the previous vertex's NEE.
-// fl / hA: the payload's flags and ray A's hit, when the caller has them
-// already (shade_batch prefetches them one path ahead).
+// The payload fields every resolve reads, and ray A (the portal estimators'
+// closest-hit ray); shade_batch loads them one path ahead.
+struct NeeIn {
+    S3 F, Li, beta;
+    float pdf, lpdf;
+    Ray rayA;
+};
+__device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot) {
+    const uint32_t N = (uint32_t)ps.n;
+    const float* nee = ps.nee;
+    NeeIn in;
+    in.F = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
+    in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+    in.beta = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
+    in.pdf = nee[kNeePdf * N + slot];
+    in.lpdf = nee[kNeeLpdf * N + slot];
+    in.rayA = load_ray6(ps.rayA, N, slot, kInf);
+    return in;
+}
+// fl / hA: the payload's flags and ray A's hit.
 template <int kFt>
 __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
-                                        int hA) {
+                                        int hA, const NeeIn& in) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
     S3 Ld = s3(0.f);
     if (fl & kNfPortal) {
         if (fl & kNfA) {
-            S3 Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+            S3 Li = in.Li;
             const int h = hA;
             if (h >= 0) {
                 int lid;
-                Li = hit_Le<kFt>(sc, h, load_ray6(ps.rayA, N, slot, kInf), &lid);
+                Li = hit_Le<kFt>(sc, h, in.rayA, &lid);
             }
-            const S3 f = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
-            if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / nee[kNeePdf * N + slot];
+            const S3 f = in.F;
+            if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / in.pdf;
         }
         if (fl & kNfDivPortal) Ld = Ld / nee[kNeePortalPdf * N + slot];
     } else if (fl & kNfMis) {
-        if ((fl & kNfC1) && hA == 0)
-            Ld = Ld + s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
+        if ((fl & kNfC1) && hA == 0) Ld = Ld + in.F;
         if (fl & kNfB) {
             const int h = ps.hitB[slot];
             const int nl = __float_as_int(nee[kNeeLight * N + slot]);
@@ -774,7 +791,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
                 Li = inf_Le(sc.lights[PT_IDX(nl, sc.n_lights)], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
             }
             if (!is_black(Li)) {
-                const S3 f2 = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+                const S3 f2 = in.Li;
                 Ld = Ld + (((f2 * Li) * s3(1.f)) * nee[kNeeSw * N + slot]) / nee[kNeeSpdf * N + slot];
             }
         }
@@ -783,16 +800,14 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
 }
 template <int kFt>
 __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
-    return nee_value<kFt>(sc, ps, slot, __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]), ps.hitA[slot]);
+    return nee_value<kFt>(sc, ps, slot, __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]), ps.hitA[slot],
+                          nee_load(ps, slot));
 }
 template <int kFt>
 __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
-                                            int hA, S3* L) {
-    const uint32_t N = (uint32_t)ps.n;
-    const float* nee = ps.nee;
-    const S3 Ld = nee_value<kFt>(sc, ps, slot, fl, hA);
-    const S3 bv = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
-    *L = *L + bv * (Ld / nee[kNeeLpdf * N + slot]);
+                                            int hA, const NeeIn& in, S3* L) {
+    const S3 Ld = nee_value<kFt>(sc, ps, slot, fl, hA, in);
+    *L = *L + in.beta * (Ld / in.lpdf);
 }
 
 __device__ __forceinline__ void put_nee(const DevPaths& ps, uint32_t slot, int k, float v) {
@@ -985,6 +1000,7 @@ struct PathPre {
     uint32_t nfl;
     S3 L, beta;
     Ray ray;
+    NeeIn nee;
 };
 __device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot, PathPre* p) {
     const uint32_t N = (uint32_t)ps.n;
@@ -996,6 +1012,7 @@ __device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot,
     p->L = load_s3(ps.L, N, slot);
     p->beta = load_s3(ps.beta, N, slot);
     p->ray = load_ray6(ps.ray, N, slot, kInf);
+    p->nee = nee_load(ps, slot);
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
@@ -1023,7 +1040,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
             }
             *ab += b;
         }
-        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, &L);
+        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.nee, &L);
         st &= ~kStNee;
     }
     if (st & kStCont) {
