@@ -459,10 +459,11 @@ __device__ __forceinline__ bool shape_test(const DevScene& sc, uint32_t flags, i
     return plane_test(sc.planes[PT_IDX(idx, sc.n_planes)], ray, t, &ph);
 }
 
+// surface_at / prim_info from the primitive's first two record words when the
+// caller has them already (k_shade loads them one path ahead)
 template <bool kSph = true>
-__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
-    float4 r0 = sc.prims[3 * PT_IDX(prim, sc.n_prims)];
-    float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
+__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, float4 r0, float4 r1, const Ray& ray,
+                                           SurfHit* si) {
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
     const pt_triangle trv = sc.tris[PT_IDX(idx, sc.n_tris)];
@@ -474,11 +475,14 @@ __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const R
     si->prim = prim;
     return ok;
 }
+template <bool kSph = true>
+__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
+    return surface_at<kSph>(sc, prim, sc.prims[3 * PT_IDX(prim, sc.n_prims)], sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1],
+                            ray, si);
+}
 
 template <bool kSph = true>
-__device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
-    float4 r0 = sc.prims[3 * PT_IDX(prim, sc.n_prims)];
-    float4 r1 = sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1];
+__device__ __forceinline__ void prim_info(const DevScene& sc, float4 r0, float4 r1, int* material, int* light) {
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
     if (kSph && (flags & kPrimSphere)) {
@@ -492,6 +496,11 @@ __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* mat
         *material = t.material;
         *light = t.area_light;
     }
+}
+template <bool kSph = true>
+__device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
+    prim_info<kSph>(sc, sc.prims[3 * PT_IDX(prim, sc.n_prims)], sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1], material,
+                    light);
 }
 
 // ----------------------------------------------------------------------------

@@ -1001,6 +1001,7 @@ struct PathPre {
     S3 L, beta;
     Ray ray;
     NeeIn nee;
+    float4 r0, r1;  // the hit primitive's record words 0-1 (loaded once `hit` is in)
 };
 __device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot, PathPre* p) {
     const uint32_t N = (uint32_t)ps.n;
@@ -1013,6 +1014,12 @@ __device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot,
     p->beta = load_s3(ps.beta, N, slot);
     p->ray = load_ray6(ps.ray, N, slot, kInf);
     p->nee = nee_load(ps, slot);
+}
+__device__ __forceinline__ void path_prefetch_prim(const DevScene& sc, PathPre* p) {
+    if ((p->st & kStCont) && p->hit >= 0) {
+        p->r0 = sc.prims[3 * PT_IDX(p->hit, sc.n_prims)];
+        p->r1 = sc.prims[3 * PT_IDX(p->hit, sc.n_prims) + 1];
+    }
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
@@ -1052,9 +1059,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         S3 beta = pre.beta;
         *ab += 24 + 4 + 12;
         SurfHit si;
-        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &si);
+        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, pre.r0, pre.r1, ray, &si);
         int mat = -1, light = -1;
-        if (found) prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
+        if (found) prim_info<Ft<kFt>::sph>(sc, pre.r0, pre.r1, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[PT_IDX(light, sc.n_lights)], si.n, -ray.d) : s3(0.f));
             else if (Ft<kFt>::inf)
@@ -1179,6 +1186,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     if (base + threadIdx.x < n) {
         slot = pq[base + threadIdx.x];
         path_prefetch(ps, slot, &pre);
+        path_prefetch_prim(sc, &pre);
     }
     if (base + stride + threadIdx.x < n) slot1 = pq[base + stride + threadIdx.x];
     for (; base < n; base += stride) {
@@ -1191,6 +1199,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         uint32_t nrays = 0;
         bool keep = false;
         if (i < n) shade_path<kFt>(sc, ps, slot, pre, rays, &nrays, &keep, &overflow, &ab);
+        if (i + stride < n) path_prefetch_prim(sc, &nxt);  // nxt.hit has arrived by now
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;
         slot1 = slot2;
