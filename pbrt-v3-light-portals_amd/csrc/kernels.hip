@@ -18,6 +18,10 @@
 namespace pt {
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// number of set bits of m below this lane (the mbcnt prefix count)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // Reserve `cnt` (0..3) consecutive queue entries per lane with one atomic per
 // wave.  Must be reached by every active lane of the wave together.
@@ -299,8 +303,14 @@ __device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray,
     return ok1 & ok2 & (tMin < ray.tmax) & (tMax > 0);
 }
 
+// PT_TRACE_PT_WAVES (experiment builds): force the waves-per-SIMD register budget
+#ifdef PT_TRACE_PT_WAVES
+#define PT_TRACE_PT_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_PT_WAVES)))
+#else
+#define PT_TRACE_PT_ATTR
+#endif
 template <bool kLdsScene, bool kSpill, bool kSph>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+__global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
                                                           int refill_min, int leaf_min, int stack_rows, int* spill,
                                                           DevStats* stats)
@@ -325,9 +335,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
     const uint32_t N = (uint32_t)ps.n;
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
-    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
-    unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
+    uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;  // per lane per launch: fit 32 bits
     bool active = false, exhausted = false, drained = false;
     uint32_t qn = 0, qe = 0;  // the wave's private chunk of the ray queue (as k_trace_nb)
     uint32_t slot = 0, kind = 0;
@@ -350,7 +359,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
                     drained = base + kTraceChunk >= n;
                 }
                 const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
-                const uint32_t k = (uint32_t)__popcll(idle & lower);
+                const uint32_t k = lanes_below(idle);
                 const uint32_t i = qn + k;
                 qn += take;
                 if (drained && qn >= qe) exhausted = true;
@@ -465,8 +474,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_pt(DevScene sc, DevPaths 
         }
     }
     flush_stats(stats, ncl, nsh, nodes, prims);
-    iters = wave_sum_u64(iters);
-    if (lane == 0 && iters) atomicAdd(&stats->lane_iters, iters);
+    const unsigned long long itw = wave_sum_u64(iters);
+    if (lane == 0 && itw) atomicAdd(&stats->lane_iters, itw);
 }
 #else
 ;
@@ -499,7 +508,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
     const uint32_t n = *rq_count;
     const uint32_t N = (uint32_t)ps.n;
     const uint32_t lane = lane_id();
-    const uint64_t lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
     bool active = false, exhausted = false, drained = false;
     // The wave takes queue entries kTraceChunk at a time (one atomic) and
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths 
                     drained = base + kTraceChunk >= n;
                 }
                 const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
-                const uint32_t k = (uint32_t)__popcll(idle & lower);
+                const uint32_t k = lanes_below(idle);
                 const uint32_t i = qn + k;
                 qn += take;
                 if (drained && qn >= qe) exhausted = true;
@@ -756,6 +764,24 @@ __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot) {
     in.pdf = nee[kNeePdf * N + slot];
     in.lpdf = nee[kNeeLpdf * N + slot];
     in.rayA = load_ray6(ps.rayA, N, slot, kInf);
+    return in;
+}
+// Only the fields the resolve of this payload reads (flags fl, ray A's hit hA):
+// what nee_value touches under the same conditions.
+__device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uint32_t fl, int hA) {
+    const uint32_t N = (uint32_t)ps.n;
+    const float* nee = ps.nee;
+    NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
+    const bool portalA = (fl & kNfPortal) && (fl & kNfA);
+    const bool mis = !(fl & kNfPortal) && (fl & kNfMis);
+    in.beta = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
+    in.lpdf = nee[kNeeLpdf * N + slot];
+    if (portalA || (mis && (fl & kNfC1) && hA == 0))
+        in.F = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
+    if ((portalA && hA < 0) || (mis && (fl & kNfB)))
+        in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
+    if (portalA) in.pdf = nee[kNeePdf * N + slot];
+    if (portalA && hA >= 0) in.rayA = load_ray6(ps.rayA, N, slot, kInf);
     return in;
 }
 // fl / hA: the payload's flags and ray A's hit.
@@ -1003,17 +1029,23 @@ struct PathPre {
     NeeIn nee;
     float4 r0, r1;  // the hit primitive's record words 0-1 (loaded once `hit` is in)
 };
-__device__ __forceinline__ void path_prefetch(const DevPaths& ps, uint32_t slot, PathPre* p) {
-    const uint32_t N = (uint32_t)ps.n;
+// Two stages: the head (state word, payload flags, hits) two paths ahead, the
+// body one path ahead and only what the head says this step will read.
+__device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t slot, PathPre* p) {
     p->st = ps.st[slot];
-    p->hidx = ps.hidx[slot];
     p->hit = ps.hit[slot];
     p->hitA = ps.hitA[slot];
-    p->nfl = __float_as_uint(ps.nee[kNeeFlags * N + slot]);
+    p->nfl = __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]);
+}
+__device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t slot, PathPre* p) {
+    const uint32_t N = (uint32_t)ps.n;
     p->L = load_s3(ps.L, N, slot);
-    p->beta = load_s3(ps.beta, N, slot);
-    p->ray = load_ray6(ps.ray, N, slot, kInf);
-    p->nee = nee_load(ps, slot);
+    if (p->st & kStCont) {
+        p->hidx = ps.hidx[slot];
+        p->beta = load_s3(ps.beta, N, slot);
+        p->ray = load_ray6(ps.ray, N, slot, kInf);
+    }
+    if (p->st & kStNee) p->nee = nee_load(ps, slot, p->nfl, p->hitA);
 }
 __device__ __forceinline__ void path_prefetch_prim(const DevScene& sc, PathPre* p) {
     if ((p->st & kStCont) && p->hit >= 0) {
@@ -1176,25 +1208,32 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     PT_WAVEQ(wq);
     uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     const uint32_t stride = gridDim.x * blockDim.x;
-    // software pipeline over the grid-stride iterations: the queue entry two
-    // paths ahead and the state of the next path are in flight while this
-    // path is shaded (slots in the queue are distinct, so no step writes what
-    // a prefetch read)
+    // software pipeline over the grid-stride iterations: while this path is
+    // shaded, the queue entry three paths ahead, the head of the path two
+    // ahead and the body of the next path are in flight (slots in the queue
+    // are distinct, so no step writes what a prefetch read)
     uint32_t base = blockIdx.x * blockDim.x;
-    uint32_t slot = 0, slot1 = 0;
-    PathPre pre{};
-    if (base + threadIdx.x < n) {
-        slot = pq[base + threadIdx.x];
-        path_prefetch(ps, slot, &pre);
+    const uint32_t i0 = base + threadIdx.x;
+    uint32_t slot = 0, slot1 = 0, slot2 = 0;
+    PathPre pre{}, nxt{};  // this path (complete) and the next one (head only)
+    if (i0 < n) {
+        slot = pq[i0];
+        path_prefetch_head(ps, slot, &pre);
+        path_prefetch_body(ps, slot, &pre);
         path_prefetch_prim(sc, &pre);
     }
-    if (base + stride + threadIdx.x < n) slot1 = pq[base + stride + threadIdx.x];
+    if (i0 + stride < n) {
+        slot1 = pq[i0 + stride];
+        path_prefetch_head(ps, slot1, &nxt);
+    }
+    if (i0 + 2 * stride < n) slot2 = pq[i0 + 2 * stride];
     for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
-        PathPre nxt{};
-        uint32_t slot2 = 0;
-        if (i + stride < n) path_prefetch(ps, slot1, &nxt);
-        if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
+        PathPre nn{};
+        uint32_t slot3 = 0;
+        if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
+        if (i + 2 * stride < n) path_prefetch_head(ps, slot2, &nn);
+        if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
         uint32_t rays[3];
         uint32_t nrays = 0;
         bool keep = false;
@@ -1203,7 +1242,9 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;
         slot1 = slot2;
+        slot2 = slot3;
         pre = nxt;
+        nxt = nn;
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
