@@ -487,8 +487,14 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
 // stack push is an unconditional LDS store above the top; the pop an
 // unconditional LDS load below it.  Only for BVHs whose stack fits in LDS.
 // ----------------------------------------------------------------------------
+// PT_TRACE_WAVES (experiment builds): force the waves-per-SIMD register budget
+#ifdef PT_TRACE_WAVES
+#define PT_TRACE_NB_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES)))
+#else
+#define PT_TRACE_NB_ATTR
+#endif
 template <bool kLdsScene, bool kSph>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_nb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+__global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
                                                           const uint32_t* __restrict__ rq_count, uint32_t* fetch,
                                                           int refill_min, int leaf_min, DevStats* stats)
 #ifdef PT_TU_TRACE
