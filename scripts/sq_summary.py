@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Summarise the SQ counter passes of scripts/gpu_pmc_sq.sh into
+profiles/<round>_sq_counters.json: per kernel, the counters summed over its
+dispatches and the ratios the DESIGN quotes (share of wave cycles spent
+waiting, instructions per wave by kind).
+
+usage: sq_summary.py --out gpurun_out --round r2 --workload "<bench workload>"
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--out", default="gpurun_out")
+ap.add_argument("--round", default="r2")
+ap.add_argument("--workload", required=True)
+ap.add_argument("--args", default="--spp 16", help="bench args the passes ran with")
+a = ap.parse_args()
+
+sums = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(set)
+for f in glob.glob(os.path.join(a.out, "pmc_sq*", "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if not ("k_shade" in k or "k_trace" in k or "k_film" in k or "k_camera" in k):
+            continue
+        sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r.get("Dispatch_Id", ""))
+
+out = {"workload": a.workload, "bench_args": a.args,
+       "method": "rocprofv3 --pmc, two passes of 8 SQ counters each (scripts/gpu_pmc_sq.sh); sums over dispatches",
+       "kernels": {}}
+for k, c in sums.items():
+    w = c.get("SQ_WAVES", 0) or 1
+    cyc = c.get("SQ_WAVE_CYCLES", 0) or 1
+    e = {"dispatches": len(disp[k]), "counters": dict(c)}
+    e["wait_any_share"] = c.get("SQ_WAIT_ANY", 0) / cyc
+    e["wait_inst_any_share"] = c.get("SQ_WAIT_INST_ANY", 0) / cyc
+    e["active_inst_any_share"] = c.get("SQ_ACTIVE_INST_ANY", 0) / cyc
+    for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM"):
+        if n in c:
+            e[n.replace("SQ_INSTS_", "insts_per_wave_").lower()] = c[n] / w
+    out["kernels"][k] = e
+    print("%-34s waves=%-9d wait_any=%.2f active_inst=%.2f valu/wave=%.0f vmem_rd/wave=%.0f" % (
+        k[-34:], w, e["wait_any_share"], e["active_inst_any_share"], e.get("insts_per_wave_valu", 0),
+        e.get("insts_per_wave_vmem_rd", 0)))
+dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", f"{a.round}_sq_counters.json")
+json.dump(out, open(dst, "w"), indent=1)
+print("wrote", os.path.relpath(dst))
