@@ -267,6 +267,7 @@ struct pt_scene {
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     int trace_bpc = 16;          // persistent trace blocks per CU
+    int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
     int leaf_min_pt = 16;        // k_trace_pt (HBM-resident BVHs): the same threshold
@@ -1091,7 +1092,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     DBuf<int> dslot;
     dslot.upload(pixslot);
     const int maxBlocksTrace = s->num_cus * 16;
-    const int maxBlocksShade = s->num_cus * 8;
+    const int maxBlocksShade = s->num_cus * s->shade_bpc;
     const bool direct = s->dev.integrator == PT_INTEGRATOR_DIRECT;
     // Batches run on `pipes` pipelines (host thread + stream + path-state
     // buffers each), dealt round-robin: while one batch traces, another
@@ -1462,6 +1463,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (v) s->shade_variant = std::atoi(v);
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
+    if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
