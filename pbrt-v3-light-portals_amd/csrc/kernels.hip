@@ -755,45 +755,42 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 // portal_arealight.cpp:29-239): the Ld of the previous vertex's NEE.
 // The payload fields every resolve reads, and ray A (the portal estimators'
 // closest-hit ray); shade_batch loads them one path ahead.
+// The payload fields a resolve reads and the traced NEE ray whose hit it
+// evaluates (ray A for the portal estimators, ray B for MIS); shade_batch
+// loads them one path ahead.
 struct NeeIn {
     S3 F, Li, beta;
     float pdf, lpdf;
-    Ray rayA;
+    int nl;   // MIS: the light the BSDF-sampled ray B must hit
+    Ray ray;
 };
-__device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot) {
-    const uint32_t N = (uint32_t)ps.n;
-    const float* nee = ps.nee;
-    NeeIn in;
-    in.F = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
-    in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
-    in.beta = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
-    in.pdf = nee[kNeePdf * N + slot];
-    in.lpdf = nee[kNeeLpdf * N + slot];
-    in.rayA = load_ray6(ps.rayA, N, slot, kInf);
-    return in;
-}
-// Only the fields the resolve of this payload reads (flags fl, ray A's hit hA):
-// what nee_value touches under the same conditions.
+// Only the fields the resolve of this payload reads (flags fl, the hits hA /
+// hB of rays A and B): what nee_value touches under the same conditions.
 __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uint32_t fl, int hA) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
-    NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
+    NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, 0, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
     const bool portalA = (fl & kNfPortal) && (fl & kNfA);
+    const bool misB = !(fl & kNfPortal) && (fl & kNfMis) && (fl & kNfB);
     const bool mis = !(fl & kNfPortal) && (fl & kNfMis);
     in.beta = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
     in.lpdf = nee[kNeeLpdf * N + slot];
     if (portalA || (mis && (fl & kNfC1) && hA == 0))
         in.F = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
-    if ((portalA && hA < 0) || (mis && (fl & kNfB)))
+    if ((portalA && hA < 0) || misB)
         in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
     if (portalA) in.pdf = nee[kNeePdf * N + slot];
-    if (portalA && hA >= 0) in.rayA = load_ray6(ps.rayA, N, slot, kInf);
+    if (portalA && hA >= 0) in.ray = load_ray6(ps.rayA, N, slot, kInf);
+    if (misB) {
+        in.nl = __float_as_int(nee[kNeeLight * N + slot]);
+        in.ray = load_ray6(ps.rayB, N, slot, kInf);
+    }
     return in;
 }
-// fl / hA: the payload's flags and ray A's hit.
+// fl / hA / hB: the payload's flags and the hits of rays A and B.
 template <int kFt>
 __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
-                                        int hA, const NeeIn& in) {
+                                        int hA, int hB, const NeeIn& in) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
     S3 Ld = s3(0.f);
@@ -803,7 +800,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
             const int h = hA;
             if (h >= 0) {
                 int lid;
-                Li = hit_Le<kFt>(sc, h, in.rayA, &lid);
+                Li = hit_Le<kFt>(sc, h, in.ray, &lid);
             }
             const S3 f = in.F;
             if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / in.pdf;
@@ -812,15 +809,15 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
     } else if (fl & kNfMis) {
         if ((fl & kNfC1) && hA == 0) Ld = Ld + in.F;
         if (fl & kNfB) {
-            const int h = ps.hitB[slot];
-            const int nl = __float_as_int(nee[kNeeLight * N + slot]);
+            const int h = hB;
+            const int nl = in.nl;
             S3 Li = s3(0.f);
             if (h >= 0) {
                 int lid;
-                const S3 le = hit_Le<kFt>(sc, h, load_ray6(ps.rayB, N, slot, kInf), &lid);
+                const S3 le = hit_Le<kFt>(sc, h, in.ray, &lid);
                 if (lid == nl) Li = le;
             } else if (Ft<kFt>::inf && sc.lights[PT_IDX(nl, sc.n_lights)].kind == PT_LIGHT_INFINITE) {
-                Li = inf_Le(sc.lights[PT_IDX(nl, sc.n_lights)], load_ray6(ps.rayB, N, slot, kInf).d);  // light.Le(ray)
+                Li = inf_Le(sc.lights[PT_IDX(nl, sc.n_lights)], in.ray.d);  // light.Le(ray)
             }
             if (!is_black(Li)) {
                 const S3 f2 = in.Li;
@@ -832,13 +829,14 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
 }
 template <int kFt>
 __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
-    return nee_value<kFt>(sc, ps, slot, __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]), ps.hitA[slot],
-                          nee_load(ps, slot));
+    const uint32_t fl = __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]);
+    const int hA = ps.hitA[slot];
+    return nee_value<kFt>(sc, ps, slot, fl, hA, ps.hitB[slot], nee_load(ps, slot, fl, hA));
 }
 template <int kFt>
 __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
-                                            int hA, const NeeIn& in, S3* L) {
-    const S3 Ld = nee_value<kFt>(sc, ps, slot, fl, hA, in);
+                                            int hA, int hB, const NeeIn& in, S3* L) {
+    const S3 Ld = nee_value<kFt>(sc, ps, slot, fl, hA, hB, in);
     *L = *L + in.beta * (Ld / in.lpdf);
 }
 
@@ -1028,7 +1026,7 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
 // of its dependent loads, and these are the first two links of the chain.
 struct PathPre {
     uint32_t st, hidx;
-    int hit, hitA;
+    int hit, hitA, hitB;
     uint32_t nfl;
     S3 L, beta;
     Ray ray;
@@ -1041,6 +1039,7 @@ __device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t 
     p->st = ps.st[slot];
     p->hit = ps.hit[slot];
     p->hitA = ps.hitA[slot];
+    p->hitB = ps.hitB[slot];
     p->nfl = __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]);
 }
 __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t slot, PathPre* p) {
@@ -1081,11 +1080,11 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 if (fl & kNfDivPortal) b += 4;
             } else if (fl & kNfMis) {
                 if (fl & kNfC1) b += 4 + 12;
-                if (fl & kNfB) b += 4 + 4 + 12 + 4 + 4 + (ps.hitB[slot] >= 0 ? 24 : 0);
+                if (fl & kNfB) b += 4 + 4 + 12 + 4 + 4 + (pre.hitB >= 0 ? 24 : 0);
             }
             *ab += b;
         }
-        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.nee, &L);
+        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.hitB, pre.nee, &L);
         st &= ~kStNee;
     }
     if (st & kStCont) {
