@@ -101,7 +101,12 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
     import pyoracle
     import ptgpu
     hs = ptgpu.HostScene(scene_path)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # Every core this process may run on, up to the box's declared CPU share
+    # (OMP_NUM_THREADS: the GPU box gives one GPU's job 16 of the host's CPUs,
+    # os.cpu_count() reports the whole machine)
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(affinity, share) if share > 0 else affinity)
     w, h = hs.film_size()
     ntiles = ((w + 15) // 16) * ((h + 15) // 16)
     stride = max(1, ntiles // (2 * threads))
@@ -115,7 +120,13 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
     _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
     rate = st["samples"] / dt / 1e6
+    host = os.cpu_count() or threads
     return {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "host_cpus": host, "affinity_cpus": affinity, "cpu_share": share or None,
+            "threads_note": (f"timed on {threads} threads: the {affinity} CPUs in this process's affinity"
+                             + (f", capped at the box's declared CPU share OMP_NUM_THREADS={share}" if share else "")
+                             + f"; the host has {host} CPUs"),
+            "all_host_cpus_linear_estimate": round(rate / threads * host, 3),
             "sample": f"every {stride}th 16x16 tile of the same frame (tiles t % {stride} == 0 over the whole image) "
                       f"at the scene's spp ({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
             "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3),
@@ -210,8 +221,7 @@ def main():
     hs = ptgpu.HostScene(spath)
     sc = ptgpu.Scene(hs, device=local, batch_slots=args.batch_slots or None)
     w, h = sc.film_size()
-    nodes, order = hs.bvh()
-    lds_scene = (32 * len(nodes) + 48 * len(order)) <= 16384  # render.hip: k_trace stages such a BVH in LDS
+    lds_scene = sc.query("trace_lds_bytes") > 0  # the library stages this BVH in LDS (PT_TRACE_LDS honoured)
     import re
     spp = int(re.search(r'"integer pixelsamples" \[(\d+)\]', open(spath).read()).group(1))
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -238,7 +248,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     agg = {"samples": 0, "closest_rays": 0, "shadow_rays": 0, "node_visits": 0, "prim_tests": 0, "trace_ms": 0.0,
-           "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0}
+           "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0, "render_ms": 0.0,
+           "reduce_ms": 0.0}
     for _ in range(args.steps):
         st = step()
         for k in agg:
@@ -258,6 +269,9 @@ def main():
         total_samples, total_rays = float(tot[0]), float(tot[1])
     else:
         total_samples, total_rays = float(agg["samples"]), float(agg["closest_rays"] + agg["shadow_rays"])
+    # every rank's own render time and film-reduce time per step (max / min on rank 0)
+    rank_times = shardmod.gather_rank_times(agg["render_ms"] / args.steps, agg["reduce_ms"] / args.steps, world,
+                                            device=f"cuda:{local}")
 
     # Kernel rooflines from one more frame with the batches run one after the
     # other (pt_set_pipelines(1)): in the timed region two pipelines overlap
@@ -265,11 +279,12 @@ def main():
     # include the co-running kernel.  This rank's shard, no collective.
     iso = {"trace_ms": 0.0, "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0,
            "node_visits": 0, "prim_tests": 0}
+    pipes = sc.query("pipelines")
     sc.set_pipelines(1)
     accum.zero_()
     st = render(my)
     torch.cuda.synchronize()
-    sc.set_pipelines(2)
+    sc.set_pipelines(pipes)
     for k in iso:
         iso[k] = st[k]
     overlapped = {"k_trace_avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4),
@@ -297,6 +312,7 @@ def main():
                        "parallelism": f"{args.shard} x{world}"},
             "mrays_per_s": round(total_rays / dt / 1e6, 2),
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
+            "rank_times": rank_times,
         }
         out.update(rooflines(iso, workload, lds_scene))
         out["roofline"]["timing"] = ("kernel launches timed with HIP events in one frame with the batches "

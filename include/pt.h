@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 8
+#define PT_ABI_VERSION 9
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -74,8 +74,16 @@ enum pt_light_kind {
     PT_LIGHT_PORTAL_AREA = 1,  /* PortalArealight on one aaplane     src/lights/portal_arealight.cpp */
     PT_LIGHT_INFINITE = 2,     /* InfiniteAreaLight, constant L (no "mapname")  src/lights/infinite.cpp */
     PT_LIGHT_DIFFUSE_SPHERE = 3, /* DiffuseAreaLight on one sphere    src/lights/diffuse.cpp, shapes/sphere.cpp */
-    PT_LIGHT_POINT = 4          /* PointLight at LightToWorld(0,0,0), L = I * scale  src/lights/point.cpp */
+    PT_LIGHT_POINT = 4,         /* PointLight at LightToWorld(0,0,0), L = I * scale  src/lights/point.cpp */
+    PT_LIGHT_DIFFUSE_PLANE = 5  /* DiffuseAreaLight on one aaplane (scenes/blender/creeper/out/creeper.pbrt:38-49):
+                                   Shape::Sample(ref) / Shape::Pdf(ref, wi)  src/core/shape.cpp:56-91 over
+                                   AAPlaneShape::Sample / Intersect  src/shapes/plane.cpp:15-72 */
 };
+
+/* Portals per PortalArealight.  The reference sizes its per-call portal
+ * distribution as a VLA (portal_arealight.cpp:42); the loader and
+ * pt_scene_create refuse more than this many with PT_ERR_UNSUPPORTED. */
+#define PT_MAX_PORTALS 64
 
 enum pt_portal_strategy {      /* PortalStrategy  src/lights/portal_arealight.h:12 */
     PT_PORTAL_LIGHT = 0,       /* "light"      SampleUniformLight */
@@ -280,6 +288,7 @@ typedef struct pt_stats {
     double shade_ms;           /* summed duration of the shading kernel */
     uint64_t shade_launches;
     uint64_t shade_bytes;      /* path integrator: algorithmic path-state bytes the shading kernel moved */
+    double reduce_ms;          /* pt_render_frame_dist: the ncclReduce of the film (HIP events on the stream) */
 } pt_stats;
 
 /* ---- host scene loader (.pbrt subset) ---- */
@@ -393,6 +402,19 @@ pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
  * and its own path-state buffers; one batch's trace kernel overlaps another's
  * shading.  1 runs the batches one after the other (isolated kernel timings). */
 pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
+
+/* Read back a setting of a device scene (what the environment overrides and
+ * the pt_set_* calls left in effect), so callers can restore or report it.
+ * PIPELINES / BATCH_SLOTS read -1 when the scene's replicas (pt_init(n > 1))
+ * do not all carry the primary's value. */
+enum pt_scene_key {
+    PT_Q_PIPELINES = 0,        /* pt_set_pipelines value (PT_PIPES) */
+    PT_Q_BATCH_SLOTS = 1,      /* pt_set_batch_slots value (0 = the default) */
+    PT_Q_TRACE_LDS_BYTES = 2,  /* bytes of BVH + primitives the trace kernel stages in LDS (0 = reads HBM) */
+    PT_Q_TRACE_SPILL = 3,      /* 1 when traversal stacks spill past the LDS rows (deep BVHs) */
+    PT_Q_FEATURES = 4          /* scene-feature set the shading kernel is instantiated for */
+};
+pt_status pt_scene_query(const pt_scene* scene, int32_t key, int64_t* value);
 
 /* Number of cropped pixels (rgb_out holds 3x this many floats). */
 pt_status pt_film_size(const pt_scene* scene, int32_t* width, int32_t* height);

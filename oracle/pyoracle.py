@@ -91,6 +91,8 @@ def film_size(desc: int) -> Tuple[int, int]:
 def _chk(rc: int) -> None:
     if rc == 3:
         raise RuntimeError("oracle: Halton dimension past the prime table (the reference CHECK-fails)")
+    if rc == 4:
+        raise RuntimeError("oracle: unsupported input (more than PT_MAX_PORTALS portals on one light)")
     if rc != 0:
         raise RuntimeError(f"oracle: error {rc}")
 

@@ -466,12 +466,15 @@ __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, float4 
                                            SurfHit* si) {
     uint32_t flags = __float_as_uint(r0.w);
     int idx = __float_as_int(r1.w);
-    const pt_triangle trv = sc.tris[PT_IDX(idx, sc.n_tris)];
-    const V3 q0 = vload3(sc.P, PT_IDX(trv.v[0], sc.n_verts)), q1 = vload3(sc.P, PT_IDX(trv.v[1], sc.n_verts)),
-             q2 = vload3(sc.P, PT_IDX(trv.v[2], sc.n_verts));
-    bool ok = (kSph && (flags & kPrimSphere)) ? sphere_surface(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, si)
-              : (flags & kPrimPlane) ? plane_surface(sc.planes[PT_IDX(idx, sc.n_planes)], ray, si)
-                                     : tri_surface(sc, idx, ray, si, q0, q1, q2);
+    bool ok;
+    if (kSph && (flags & kPrimSphere)) ok = sphere_surface(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, si);
+    else if (flags & kPrimPlane) ok = plane_surface(sc.planes[PT_IDX(idx, sc.n_planes)], ray, si);
+    else {  // a triangle record: only here is idx a triangle index (analytic records hold a shape index)
+        const pt_triangle trv = sc.tris[PT_IDX(idx, sc.n_tris)];
+        const V3 q0 = vload3(sc.P, PT_IDX(trv.v[0], sc.n_verts)), q1 = vload3(sc.P, PT_IDX(trv.v[1], sc.n_verts)),
+                 q2 = vload3(sc.P, PT_IDX(trv.v[2], sc.n_verts));
+        ok = tri_surface(sc, idx, ray, si, q0, q1, q2);
+    }
     si->prim = prim;
     return ok;
 }

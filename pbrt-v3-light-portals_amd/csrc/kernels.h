@@ -21,7 +21,7 @@ constexpr int kNodeSteps = PT_NODE_STEPS;
 constexpr int kLeafSteps = PT_LEAF_STEPS;
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
-constexpr int kMaxPortals = 64;
+constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h
 constexpr int kLdsSceneMax = 16384;  // bytes of BVH nodes + prim records staged in LDS by k_trace<true>
 
 // HaltonSampler constants for the per-pixel offset (halton.cpp:65-93)

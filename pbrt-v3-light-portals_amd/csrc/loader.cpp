@@ -1007,7 +1007,16 @@ class Loader {
                     L.kind = PT_LIGHT_PORTAL_AREA;
                     portal_params(gs_.areaLightParams, &L);
                 } else if (gs_.areaLight == "diffuse" || gs_.areaLight == "area") {
-                    throw PtError(PT_ERR_UNSUPPORTED, "diffuse area light on an aaplane is outside the supported subset");
+                    // MakeAreaLight "diffuse" on an AAPlaneShape (api.cpp:768-786, creeper.pbrt:38-49):
+                    // a DiffuseAreaLight sampled through Shape::Sample(ref) / Shape::Pdf(ref, wi)
+                    // (shape.cpp:56-91) over the plane's own Sample / Intersect (plane.cpp:15-72);
+                    // parameters it does not read ("strategy", "portalData") are ignored as the
+                    // reference's ParamSet does (unused-parameter warning only)
+                    if (out_->spectral)
+                        throw PtError(PT_ERR_UNSUPPORTED, "aaplane area lights in a SampledSpectrum (hero) scene");
+                    L.kind = PT_LIGHT_DIFFUSE_PLANE;
+                    diffuse_params(gs_.areaLightParams, &L);
+                    L.first_portal = 0; L.n_portals = 0;
                 } else
                     throw PtError(PT_ERR_UNSUPPORTED, "area light \"" + gs_.areaLight + "\"");
                 L.shape = pidx;
@@ -1099,7 +1108,9 @@ class Loader {
             out_->portals.push_back(p);
             L->n_portals++;
         }
-        if (L->n_portals > 64) throw PtError(PT_ERR_UNSUPPORTED, "more than 64 portals on one light");
+        if (L->n_portals > PT_MAX_PORTALS)
+            throw PtError(PT_ERR_UNSUPPORTED, "more than PT_MAX_PORTALS (" + std::to_string(PT_MAX_PORTALS) +
+                                                  ") portals on one light");
     }
 
     static void parse_portal_sexpr(const std::string& s, std::vector<std::vector<std::string>>* out) {

@@ -277,6 +277,12 @@ struct pt_scene {
     // (same scene, same host-built BVH), rendered by one host thread each
     std::vector<std::unique_ptr<pt_scene>> replicas;
     std::vector<int> devices;  // ids[0..n) the scene was created for (primary first)
+    ~pt_scene() {
+        // replicas first (each makes its own device current), then this scene's streams and buffers are
+        // freed with its own device current
+        replicas.clear();
+        (void)hipSetDevice(device);
+    }
 };
 
 // Multi-process communicator (pt_comm_create): RCCL over the GPUs of the job
@@ -458,7 +464,8 @@ static void build_hero(pt_scene* s, const pt_scene_desc* d, const std::vector<De
                        const std::vector<float>& area, const std::vector<DevSphere>& spheres) {
     if (!d->material_s60 || !d->light_s60) throw PtError(PT_ERR_INVALID_ARG, "spectral scene without 60-bin tables");
     for (int i = 0; i < d->n_lights; ++i)
-        if (d->lights[i].kind == PT_LIGHT_PORTAL_AREA || d->lights[i].kind == PT_LIGHT_POINT)
+        if (d->lights[i].kind == PT_LIGHT_PORTAL_AREA || d->lights[i].kind == PT_LIGHT_POINT ||
+            d->lights[i].kind == PT_LIGHT_DIFFUSE_PLANE)
             throw PtError(PT_ERR_UNSUPPORTED, "hero integrators support area and infinite lights");
     const SpecTables60& t = spectral_tables();
     std::vector<float> xyz(3 * kNSpec), illum(7 * kNSpec);
@@ -607,10 +614,14 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
             if (l.shape < 0 || l.shape >= d->n_triangles) throw PtError(PT_ERR_INVALID_ARG, "bad light shape");
         } else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
             if (l.shape < 0 || l.shape >= d->n_spheres) throw PtError(PT_ERR_INVALID_ARG, "bad sphere light shape");
+        } else if (l.kind == PT_LIGHT_DIFFUSE_PLANE) {
+            if (l.shape < 0 || l.shape >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad plane light shape");
         } else if (l.kind == PT_LIGHT_PORTAL_AREA) {
             if (l.shape < 0 || l.shape >= d->n_planes) throw PtError(PT_ERR_INVALID_ARG, "bad portal light shape");
-            if (l.n_portals < 0 || l.n_portals > kMaxPortals || l.first_portal < 0 ||
-                l.first_portal + l.n_portals > d->n_portals)
+            if (l.n_portals > kMaxPortals)
+                throw PtError(PT_ERR_UNSUPPORTED, "more than PT_MAX_PORTALS (" + std::to_string(kMaxPortals) +
+                                                      ") portals on one light");
+            if (l.n_portals < 0 || l.first_portal < 0 || l.first_portal + l.n_portals > d->n_portals)
                 throw PtError(PT_ERR_INVALID_ARG, "bad portal range");
         } else if (l.kind != PT_LIGHT_INFINITE && l.kind != PT_LIGHT_POINT)
             throw PtError(PT_ERR_UNSUPPORTED, "unsupported light kind");
@@ -1381,6 +1392,7 @@ static void fill_stats(const RenderResult& r, pt_stats* st) {
     st->shade_ms = r.shade_ms;
     st->shade_launches = r.shade_launches;
     st->shade_bytes = r.st.shade_bytes;
+    st->reduce_ms = 0;
 }
 
 template <class F>
@@ -1549,6 +1561,26 @@ using namespace pt;
 extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+pt_status pt_scene_query(const pt_scene* s, int32_t key, int64_t* value) {
+    return guarded([&] {
+        if (!s || !value) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        switch (key) {
+            case PT_Q_PIPELINES:  // -1 when a replica (pt_init(n > 1)) differs from the primary
+                *value = s->pipes;
+                for (auto& r : s->replicas) if (r->pipes != s->pipes) *value = -1;
+                break;
+            case PT_Q_BATCH_SLOTS:
+                *value = (int64_t)s->target_slots;
+                for (auto& r : s->replicas) if (r->target_slots != s->target_slots) *value = -1;
+                break;
+            case PT_Q_TRACE_LDS_BYTES: *value = (int64_t)s->lds_scene_bytes; break;
+            case PT_Q_TRACE_SPILL: *value = s->trace_spill; break;
+            case PT_Q_FEATURES: *value = s->features; break;
+            default: throw PtError(PT_ERR_INVALID_ARG, "unknown pt_scene_query key");
+        }
+    });
+}
 const char* pt_last_error(void) { return g_last_error.c_str(); }
 
 pt_status pt_load_pbrt(const char* path, pt_host_scene** out) {
@@ -1636,8 +1668,21 @@ pt_status pt_render_frame_dist(pt_scene* s, pt_comm* comm, float* d_accum, void*
         const size_t np = (size_t)s->fr.width() * s->fr.height();
         HIPCHK(hipMemsetAsync(d_accum, 0, np * sizeof(float4), (hipStream_t)stream));
         RenderResult r = render_tiles(s, comm->rank, comm->nranks, 0, s->spp, (float4*)d_accum, (hipStream_t)stream);
+        // the frame's one collective, bracketed by events on its stream: reduce_ms is this rank's wait for
+        // the slowest rank plus the transfer, the figure that tells tail imbalance from reduce cost
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, (hipStream_t)stream));
         NCCLCHK(ncclReduce(d_accum, d_accum, 4 * np, ncclFloat, ncclSum, 0, comm->comm, (hipStream_t)stream));
+        HIPCHK(hipEventRecord(e1, (hipStream_t)stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
         fill_stats(r, stats);
+        if (stats) stats->reduce_ms = ms;
     });
 }
 
@@ -1795,10 +1840,15 @@ pt_status pt_render(pt_scene* s, float* rgb_out, pt_stats* stats) {
 pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
     return guarded([&] {
         if (!s || slots <= 0) throw PtError(PT_ERR_INVALID_ARG, "bad argument");
+        // every replica (pt_init(n > 1)) gets the same batch size, checked against its own limit
         if ((uint64_t)slots > slot_limit(s))
             throw PtError(PT_ERR_INVALID_ARG, "batch slots exceed the 32-bit path-state indexing limit (" +
                                                   std::to_string(slot_limit(s)) + ")");
+        for (auto& r : s->replicas)
+            if ((uint64_t)slots > slot_limit(r.get()))
+                throw PtError(PT_ERR_INVALID_ARG, "batch slots exceed a replica's path-state indexing limit");
         s->target_slots = (size_t)slots;
+        for (auto& r : s->replicas) r->target_slots = (size_t)slots;
     });
 }
 

@@ -38,7 +38,8 @@ class pt_stats(ctypes.Structure):
                 ("prim_tests", ctypes.c_uint64), ("samples", ctypes.c_uint64),
                 ("render_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("trace_launches", ctypes.c_uint64), ("shade_ms", ctypes.c_double),
-                ("shade_launches", ctypes.c_uint64), ("shade_bytes", ctypes.c_uint64)]
+                ("shade_launches", ctypes.c_uint64), ("shade_bytes", ctypes.c_uint64),
+                ("reduce_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -89,6 +90,7 @@ def lib() -> ctypes.CDLL:
     L.pt_film_size_host.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.pt_set_batch_slots.argtypes = [vp, ctypes.c_int64]
     L.pt_set_pipelines.argtypes = [vp, ctypes.c_int32]
+    L.pt_scene_query.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
     L.pt_write_pfm.argtypes = [ctypes.c_char_p, f32p, i32, i32]
     L.pt_write_image.argtypes = [ctypes.c_char_p, f32p, i32, i32, i32, i32, i32, i32]
     L.pt_write_film_image.argtypes = [vp, ctypes.c_char_p, f32p]
@@ -311,6 +313,15 @@ class Scene:
     def set_pipelines(self, n: int) -> None:
         """pt_set_pipelines: batches in flight (1 = one after the other)."""
         _check(lib().pt_set_pipelines(self._s, int(n)))
+
+    QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4}
+
+    def query(self, key: str) -> int:
+        """pt_scene_query: a setting in effect (pipelines, batch_slots,
+        trace_lds_bytes, trace_spill, features)."""
+        v = ctypes.c_int64()
+        _check(lib().pt_scene_query(self._s, self.QUERY_KEYS[key], ctypes.byref(v)))
+        return v.value
 
     @property
     def handle(self) -> int:

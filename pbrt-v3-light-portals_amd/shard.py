@@ -90,5 +90,35 @@ def reduce_to_root(accum) -> None:
     dist.reduce(accum, dst=0)
 
 
+def summarize_rank_times(per_rank) -> dict:
+    """Per-step timing of every rank, so a scaling run can tell tail imbalance
+    (one rank's tiles taking longer) from the cost of the frame's one
+    collective.  per_rank: [(render_ms, reduce_ms), ...] in rank order --
+    render_ms is the rank's own device render time of its shard, reduce_ms its
+    ncclReduce of the film (HIP events around it: the wait for the slowest
+    rank plus the transfer)."""
+    rend = [float(r) for r, _ in per_rank]
+    red = [float(x) for _, x in per_rank]
+    mean = sum(rend) / len(rend)
+    return {"ranks": len(per_rank),
+            "render_ms_per_step": {"max": round(max(rend), 3), "min": round(min(rend), 3), "mean": round(mean, 3)},
+            "render_imbalance": round(max(rend) / mean, 4) if mean > 0 else None,
+            "reduce_ms_per_step": {"max": round(max(red), 3), "min": round(min(red), 3)},
+            "per_rank_render_ms": [round(v, 3) for v in rend]}
+
+
+def gather_rank_times(render_ms: float, reduce_ms: float, world: int, device="cpu") -> Optional[dict]:
+    """All-gather (render_ms, reduce_ms) of every rank; the summary on every
+    rank (world 1: this process alone, no collective)."""
+    if world <= 1:
+        return summarize_rank_times([(render_ms, reduce_ms)])
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([render_ms, reduce_ms], dtype=torch.float64, device=device)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    return summarize_rank_times([(float(t[0]), float(t[1])) for t in every])
+
+
 def scaling(mode: str) -> str:
     return "weak" if mode == "samples" else "strong"

@@ -6,6 +6,13 @@
   scenes/lamp/lamp.pbrt             the reference's one portal scene (scenes/blender/lamp/out/lamp.pbrt:
                                     two axis-2 portals, one '+'-facing, plymesh, matte + metal)
   scenes/lamp/meshes/00001/*.ply    its meshes (binary little-endian PLY, byte-identical copies)
+  scenes/creeper/creeper.pbrt       scenes/blender/creeper/out/creeper.pbrt: DiffuseAreaLight on an axis-1
+                                    aaplane (carrying unused "portalData" with five '+' portals), a point
+                                    light, Scale -1 1 1 before LookAt, DirectLighting
+  scenes/creeper/sandbox.pbrt       scenes/blender/creeper/out/sandbox.pbrt: PortalArealight under a rotated
+                                    Transform, five axis-2 '+' portals, strategy projection, DirectLighting
+  scenes/creeper/test00001.pbrt     scenes/blender/creeper/out/test00001.pbrt: path, trianglemesh emitter
+  scenes/creeper/meshes/00001/*.ply their meshes (byte-identical copies)
 Scene files are renderer inputs (fixtures), not source; a provenance comment is
 prepended to each text file."""
 import os
@@ -16,9 +23,14 @@ DST = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scenes")
 
 TEXT = [("killeroo-simple.pbrt", "killeroo-simple.pbrt"),
         ("geometry/killeroo.pbrt", "geometry/killeroo.pbrt"),
-        ("blender/lamp/out/lamp.pbrt", "lamp/lamp.pbrt")]
+        ("blender/lamp/out/lamp.pbrt", "lamp/lamp.pbrt"),
+        ("blender/creeper/out/creeper.pbrt", "creeper/creeper.pbrt"),
+        ("blender/creeper/out/sandbox.pbrt", "creeper/sandbox.pbrt"),
+        ("blender/creeper/out/test00001.pbrt", "creeper/test00001.pbrt")]
 BINARY = [("blender/lamp/out/meshes/00001/%s.ply" % m, "lamp/meshes/00001/%s.ply" % m)
           for m in ("Base_mat0", "Lampshade_mat0", "Leg_mat0", "Room_mat1", "Room_mat2")]
+BINARY += [("blender/creeper/out/meshes/00001/%s.ply" % m, "creeper/meshes/00001/%s.ply" % m)
+           for m in ("Cube_mat0", "Ground_mat0", "creeper.001_mat0", "creeper_mat0")]
 
 for rel, dst in TEXT:
     out = os.path.join(DST, dst)

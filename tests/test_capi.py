@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ptgpu.lib().pt_abi_version() == 8
+    assert ptgpu.lib().pt_abi_version() == 9
 
 
 def test_pt_h_compiles_as_c():
@@ -65,13 +65,17 @@ def test_ctypes_mirror_matches_c_layout():
         src = os.path.join(d, "t.c")
         open(src, "w").write('#include <stdio.h>\n#include <stddef.h>\n#include "pt.h"\nint main(void){printf("%zu %zu %zu %zu",'
                              ' sizeof(pt_scene_desc), offsetof(pt_scene_desc, integrator), '
-                             'offsetof(pt_scene_desc, n_spheres), sizeof(pt_material));return 0;}\n')
+                             'offsetof(pt_scene_desc, n_spheres), sizeof(pt_material));'
+                             'printf(" %zu %zu %zu", sizeof(pt_stats), offsetof(pt_stats, reduce_ms), sizeof(pt_light));'
+                             'return 0;}\n')
         exe = os.path.join(d, "t")
         subprocess.check_call(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), src, "-o", exe])
         got = [int(x) for x in subprocess.check_output([exe]).split()]
     import ctypes
     D = ptgpu.pt_scene_desc
-    assert got == [ctypes.sizeof(D), D.integrator.offset, D.n_spheres.offset, ctypes.sizeof(ptgpu.pt_material)]
+    assert got[:4] == [ctypes.sizeof(D), D.integrator.offset, D.n_spheres.offset, ctypes.sizeof(ptgpu.pt_material)]
+    S = ptgpu.pt_stats
+    assert got[4:] == [ctypes.sizeof(S), S.reduce_ms.offset, 168]  # tests index pt_light records as 42 int32
 
 
 def test_bvh_host_capacities(tmp_path):
@@ -103,4 +107,5 @@ def test_multi_gpu_entry_points_reject_bad_arguments():
     assert L.pt_comm_create(0, 0, None, None) == 1
     assert L.pt_film_reduce(None, None, None, 0, None) == 1
     assert L.pt_render_frame_dist(None, None, None, None, None) == 1
+    assert L.pt_scene_query(None, 0, None) == 1
     assert L.pt_shutdown() == 0

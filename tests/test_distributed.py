@@ -43,10 +43,19 @@ def _worker(rank, world, port, scene, spp, mode, out):
             accum.add_(torch.from_numpy(acc))
             return st
 
-        st = sh.render_frame(my, render, accum, sh.reduce_to_root)
+        import time
+        t0 = time.perf_counter()
+        st = sh.render_frame(my, render, accum, None)
+        t1 = time.perf_counter()
+        sh.reduce_to_root(accum)
+        t2 = time.perf_counter()
+        # bench.py's per-rank diagnostics: every rank's render and reduce time, gathered
+        times = sh.gather_rank_times((t1 - t0) * 1e3, (t2 - t1) * 1e3, world)
         n = torch.tensor([st["samples"]], dtype=torch.float64)
         dist.all_reduce(n)
         if rank == 0:
+            import json
+            json.dump(times, open(out + ".times.json", "w"))
             np.save(out, accum.numpy())
             np.save(out + ".rgb.npy", hs.resolve(accum.numpy()))
             np.save(out + ".n.npy", n.numpy())
@@ -59,6 +68,12 @@ def _run(tmp_path, mode, world=2):
     out = str(tmp_path / f"film_{mode}.npy")
     mp.start_processes(_worker, args=(world, _free_port(), scene, 4, mode, out), nprocs=world, join=True,
                        start_method="spawn")
+    import json
+    times = json.load(open(out + ".times.json"))
+    assert times["ranks"] == world and len(times["per_rank_render_ms"]) == world
+    for k in ("render_ms_per_step", "reduce_ms_per_step"):
+        assert times[k]["max"] >= times[k]["min"] >= 0
+    assert times["render_imbalance"] >= 1.0
     return scene, np.load(out), np.load(out + ".rgb.npy"), float(np.load(out + ".n.npy")[0])
 
 
@@ -98,6 +113,16 @@ def test_two_rank_frame_matches_single_process(tmp_path, mode):
         # spp unchanged: the resolved frame is the reference render itself
         img, _ = pyoracle.render(hs.desc, nthreads=4)
         np.testing.assert_allclose(rgb, img, rtol=2e-6, atol=1e-7)
+
+
+def test_rank_time_summary():
+    """bench.py's multi-rank diagnostics (shard.summarize_rank_times): max / min
+    render time, imbalance and reduce time of every rank."""
+    t = shard.summarize_rank_times([(100.0, 5.0), (120.0, 1.0)])
+    assert t["render_ms_per_step"] == {"max": 120.0, "min": 100.0, "mean": 110.0}
+    assert t["reduce_ms_per_step"] == {"max": 5.0, "min": 1.0}
+    assert abs(t["render_imbalance"] - 120 / 110) < 1e-3
+    assert shard.gather_rank_times(7.0, 0.0, 1)["per_rank_render_ms"] == [7.0]
 
 
 def test_host_resolve_matches_oracle_writeimage(tmp_path):

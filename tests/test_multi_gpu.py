@@ -50,6 +50,22 @@ def test_replicas_match_single_device(tmp_path, ndev):
     _close(many, one)
 
 
+def test_replicas_take_batch_and_pipeline_settings(tmp_path):
+    """pt_set_batch_slots / pt_set_pipelines reach every replica (the query
+    reads -1 when a replica differs); a small batch on two replicas renders
+    the single-device frame."""
+    import ptgpu
+    hs = ptgpu.HostScene(scene_variant(tmp_path, res=(72, 40), spp=8))
+    one, st1 = ptgpu.Scene(hs, device=0).render()
+    sc = ptgpu.Scene(hs, devices=[0, 0], batch_slots=4096)
+    sc.set_pipelines(3)
+    assert sc.query("batch_slots") == 4096
+    assert sc.query("pipelines") == 3
+    many, stn = sc.render()
+    _same_counts(st1, stn)
+    _close(many, one)
+
+
 def _worker(rank, world, port, scene, out, mode):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +87,7 @@ def _worker(rank, world, port, scene, out, mode):
             comm = ptgpu.Comm(world, rank, ptgpu.comm_unique_id())
             st = comm.render_frame(sc, acc.data_ptr(), 0)
             torch.cuda.synchronize()
+            assert st["reduce_ms"] > 0 and st["render_ms"] > 0  # bench.py's per-rank diagnostics
             film = acc.cpu()
             comm.close()
         else:
