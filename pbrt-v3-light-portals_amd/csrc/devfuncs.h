@@ -26,8 +26,7 @@ __device__ __forceinline__ float radical_inverse_base3(uint32_t a) {  // lowdisc
 }
 
 template <typename Rev>
-__device__ __forceinline__ float scrambled_ri_digits(const DevScene& sc, int dim, uint32_t a, const DivMagic& dm,
-                                                     const uint16_t* perm) {
+__device__ __forceinline__ float scrambled_ri_digits(float c0, uint32_t a, const DivMagic& dm, const uint16_t* perm) {
     Rev rev = 0;
     float invBaseN = 1;
     // Digits four at a time: the digit chain is ALU only, so the four
@@ -54,16 +53,18 @@ __device__ __forceinline__ float scrambled_ri_digits(const DevScene& sc, int dim
             }
         }
     }
-    return smin(invBaseN * ((float)rev + sc.perm_c0[dim]), kOneMinusEps);
+    return smin(invBaseN * ((float)rev + c0), kOneMinusEps);
 }
 
-__device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, int dim, uint32_t a) {  // :405-424
-    const DivMagic dm = sc.divs[dim];
-    const uint16_t* perm = sc.perm + sc.prime_sums[dim];
+__device__ __forceinline__ float scrambled_radical_inverse(const DivMagic& dm, const uint16_t* perm, float c0,
+                                                           uint32_t a) {  // :405-424
     // reversedDigits < base^nDigits <= base * a: with base * a < 2^32 the
     // reference's 64-bit accumulator never leaves 32 bits (same value, same float)
-    if ((uint64_t)a * dm.base < (1ull << 32)) return scrambled_ri_digits<uint32_t>(sc, dim, a, dm, perm);
-    return scrambled_ri_digits<uint64_t>(sc, dim, a, dm, perm);
+    if ((uint64_t)a * dm.base < (1ull << 32)) return scrambled_ri_digits<uint32_t>(c0, a, dm, perm);
+    return scrambled_ri_digits<uint64_t>(c0, a, dm, perm);
+}
+__device__ __forceinline__ float scrambled_radical_inverse(const DevScene& sc, int dim, uint32_t a) {
+    return scrambled_radical_inverse(sc.divs[dim], sc.perm + sc.prime_sums[dim], sc.perm_c0[dim], a);
 }
 
 // dim must be < sc.max_dim (checked by the caller).
@@ -72,6 +73,39 @@ __device__ __forceinline__ float halton_dim(const DevScene& sc, uint32_t idx, in
     if (dim == 0) return (float)reverse_bits32(idx >> sc.hal_exp0) * 0x1p-32f;  // RadicalInverse(0, .)
     if (dim == 1) return radical_inverse_base3(fast_div(idx, sc.div_scale1));
     return scrambled_radical_inverse(sc, dim, idx);
+}
+
+// The Halton tables of the leading DevScene::hal_lds_dims dimensions staged in
+// LDS by the shading kernel (the digit loop's permutation gathers are its
+// longest chain of dependent loads): per dimension {magic, base | first
+// permutation entry << 16, shift, 1/base} and c0, then those dimensions'
+// permutation entries.
+struct HalLds {
+    const uint4* rec;
+    const float* c0;
+    const uint16_t* perm;
+    int dims;
+};
+__device__ __forceinline__ HalLds stage_halton(const DevScene& sc, uint4* lds) {
+    const int D = sc.hal_lds_dims;
+    uint4* rec = lds;
+    float* c0 = (float*)(lds + D);
+    uint16_t* perm = (uint16_t*)(c0 + D);
+    for (int i = threadIdx.x; i < D; i += blockDim.x) {
+        const DivMagic dm = sc.divs[i];
+        rec[i] = make_uint4(dm.magic, dm.base | ((uint32_t)sc.prime_sums[i] << 16), dm.shift, __float_as_uint(dm.inv_base));
+        c0[i] = sc.perm_c0[i];
+    }
+    for (int i = threadIdx.x; i < sc.hal_lds_perm; i += blockDim.x) perm[i] = sc.perm[i];
+    __syncthreads();
+    return HalLds{rec, c0, perm, D};
+}
+// halton_dim with the staged tables for dimensions below hl.dims.
+__device__ __forceinline__ float halton_dim(const DevScene& sc, const HalLds& hl, uint32_t idx, int dim) {
+    if (dim < 2 || dim >= hl.dims) return halton_dim(sc, idx, dim);
+    const uint4 r = hl.rec[dim];
+    const DivMagic dm{r.y & 0xffffu, r.x, r.z, __uint_as_float(r.w)};
+    return scrambled_radical_inverse(dm, hl.perm + (r.y >> 16), hl.c0[dim], idx);
 }
 
 // Per-pixel Halton offset (halton.cpp:96-113); values stay far below 2^32.
@@ -248,9 +282,13 @@ __device__ __forceinline__ V3 vload3(const float* a, int i) { return v3(a[3 * i]
 // (triangle.cpp:297-420, interaction.cpp:44-89).  Returns false when the
 // reference would reject (it never does for the primitive that won in the
 // traversal, which already applied the same tests).
-__device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, const Ray& ray, SurfHit* si, V3 p0, V3 p1,
-                                            V3 p2) {
-    const pt_triangle tr = sc.tris[PT_IDX(ti, sc.n_tris)];
+// trflags: the triangle's PT_TRI_* flags; its index record (uv / normal /
+// tangent vertex indices) is read only when the mesh carries one of them.
+__device__ __forceinline__ bool tri_surface(const DevScene& sc, int ti, uint32_t trflags, const Ray& ray, SurfHit* si,
+                                            V3 p0, V3 p1, V3 p2) {
+    pt_triangle tr;
+    tr.flags = trflags;
+    if (trflags & (PT_TRI_HAS_UV | PT_TRI_HAS_N | PT_TRI_HAS_S)) tr = sc.tris[PT_IDX(ti, sc.n_tris)];
     Ray r2 = ray;
     r2.tmax = kInf;
     float t, b0, b1, b2;
@@ -461,33 +499,47 @@ __device__ __forceinline__ bool shape_test(const DevScene& sc, uint32_t flags, i
 
 // surface_at / prim_info from the primitive's first two record words when the
 // caller has them already (k_shade loads them one path ahead)
+// A primitive's 48-byte record (BVH order): words 0-2 .xyz hold a
+// triangle's world vertices -- the same floats as the vertex array
+// (TriangleMesh, triangle.cpp:75) -- and the .w words its flags, shape index
+// and packed material / area light (device.h kPrimTriShift, prim_info_word).
+struct PrimRec {
+    float4 r0, r1, r2;
+};
+__device__ __forceinline__ PrimRec prim_rec(const DevScene& sc, int prim) {
+    const float4* p = sc.prims + 3 * PT_IDX(prim, sc.n_prims);
+    return PrimRec{p[0], p[1], p[2]};
+}
+
 template <bool kSph = true>
-__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, float4 r0, float4 r1, const Ray& ray,
+__device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const PrimRec& rec, const Ray& ray,
                                            SurfHit* si) {
-    uint32_t flags = __float_as_uint(r0.w);
-    int idx = __float_as_int(r1.w);
+    uint32_t flags = __float_as_uint(rec.r0.w);
+    int idx = __float_as_int(rec.r1.w);
     bool ok;
     if (kSph && (flags & kPrimSphere)) ok = sphere_surface(sc.spheres[PT_IDX(idx, sc.n_spheres)], ray, si);
     else if (flags & kPrimPlane) ok = plane_surface(sc.planes[PT_IDX(idx, sc.n_planes)], ray, si);
-    else {  // a triangle record: only here is idx a triangle index (analytic records hold a shape index)
-        const pt_triangle trv = sc.tris[PT_IDX(idx, sc.n_tris)];
-        const V3 q0 = vload3(sc.P, PT_IDX(trv.v[0], sc.n_verts)), q1 = vload3(sc.P, PT_IDX(trv.v[1], sc.n_verts)),
-                 q2 = vload3(sc.P, PT_IDX(trv.v[2], sc.n_verts));
-        ok = tri_surface(sc, idx, ray, si, q0, q1, q2);
-    }
+    else  // a triangle record: only here is idx a triangle index (analytic records hold a shape index)
+        ok = tri_surface(sc, idx, (flags >> kPrimTriShift) & 31u, ray, si, v3(rec.r0.x, rec.r0.y, rec.r0.z),
+                         v3(rec.r1.x, rec.r1.y, rec.r1.z), v3(rec.r2.x, rec.r2.y, rec.r2.z));
     si->prim = prim;
     return ok;
 }
 template <bool kSph = true>
 __device__ __forceinline__ bool surface_at(const DevScene& sc, int prim, const Ray& ray, SurfHit* si) {
-    return surface_at<kSph>(sc, prim, sc.prims[3 * PT_IDX(prim, sc.n_prims)], sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1],
-                            ray, si);
+    return surface_at<kSph>(sc, prim, prim_rec(sc, prim), ray, si);
 }
 
 template <bool kSph = true>
-__device__ __forceinline__ void prim_info(const DevScene& sc, float4 r0, float4 r1, int* material, int* light) {
-    uint32_t flags = __float_as_uint(r0.w);
-    int idx = __float_as_int(r1.w);
+__device__ __forceinline__ void prim_info(const DevScene& sc, const PrimRec& rec, int* material, int* light) {
+    uint32_t flags = __float_as_uint(rec.r0.w);
+    if (!(flags & kPrimInfoTable)) {  // GeometricPrimitive's material / area light from the record
+        const uint32_t w = __float_as_uint(rec.r2.w);
+        *material = (int)(w & 0xffffu);
+        *light = (int)(w >> 16) - 1;
+        return;
+    }
+    int idx = __float_as_int(rec.r1.w);
     if (kSph && (flags & kPrimSphere)) {
         *material = sc.spheres[PT_IDX(idx, sc.n_spheres)].material;
         *light = sc.spheres[PT_IDX(idx, sc.n_spheres)].area_light;
@@ -502,8 +554,7 @@ __device__ __forceinline__ void prim_info(const DevScene& sc, float4 r0, float4 
 }
 template <bool kSph = true>
 __device__ __forceinline__ void prim_info(const DevScene& sc, int prim, int* material, int* light) {
-    prim_info<kSph>(sc, sc.prims[3 * PT_IDX(prim, sc.n_prims)], sc.prims[3 * PT_IDX(prim, sc.n_prims) + 1], material,
-                    light);
+    prim_info<kSph>(sc, prim_rec(sc, prim), material, light);
 }
 
 // ----------------------------------------------------------------------------
@@ -1223,7 +1274,7 @@ __device__ __forceinline__ float area_pdf_li(const DevScene& sc, const DevLight&
     } else if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
         // Triangle::Intersect on this one triangle (tMax = Infinity).
         const pt_triangle tr = sc.tris[PT_IDX(l.shape, sc.n_tris)];
-        ok = tri_surface(sc, l.shape, r, &isl, vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)),
+        ok = tri_surface(sc, l.shape, tr.flags, r, &isl, vload3(sc.P, PT_IDX(tr.v[0], sc.n_verts)),
                          vload3(sc.P, PT_IDX(tr.v[1], sc.n_verts)), vload3(sc.P, PT_IDX(tr.v[2], sc.n_verts)));
     } else {
         ok = plane_surface(sc.planes[PT_IDX(l.shape, sc.n_planes)], r, &isl);

@@ -62,6 +62,19 @@ constexpr uint32_t kPrimPlane = 1u;       // AAPlaneShape (else Triangle)
 constexpr uint32_t kPrimDegenerate = 2u;  // Triangle::Intersect always rejects (triangle.cpp:309-315)
 constexpr uint32_t kPrimSphere = 4u;      // Sphere
 constexpr uint32_t kPrimAnalytic = kPrimPlane | kPrimSphere;  // record holds a shape index, not vertices
+constexpr uint32_t kPrimInfoTable = 8u;   // material / area light too large for word 2 .w: read the shape table
+// The shading step reads everything the reference's GeometricPrimitive /
+// Triangle hands it for a C2-style mesh from the record itself: bits 8-12 of
+// word 0 .w carry the triangle's PT_TRI_* flags, word 2 .w the material
+// (bits 0-15) and area light + 1 (bits 16-31), so a hit needs no triangle
+// table or vertex-array load unless the mesh has uv / normals / tangents.
+constexpr uint32_t kPrimTriShift = 8u;
+__host__ __device__ constexpr uint32_t prim_info_word(int material, int light) {
+    return (uint32_t)(material & 0xffff) | ((uint32_t)(light + 1) << 16);
+}
+__host__ __device__ constexpr bool prim_info_fits(int material, int light) {
+    return material >= 0 && material < 0xffff && light >= -1 && light + 1 < 0xffff;
+}
 
 // PT_GUARDS (diagnostic build, `make guard`): scene-table indices on the
 // shading path are range-checked; the first failing check records
@@ -107,6 +120,8 @@ struct DevScene {
     const DivMagic* divs;   // per dimension: prime base, magic, shift, 1/base
     const float* perm_c0;   // per dimension: invBase * perm[0] / (1 - invBase)
     int max_dim;
+    int hal_lds_dims;       // leading dimensions whose tables the shading kernel stages in LDS (0: none)
+    int hal_lds_perm;       // their permutation entries (prime_sums[hal_lds_dims])
     int hal_exp0;
     uint32_t hal_scale1;
     DivMagic div_scale1;

@@ -726,6 +726,18 @@ struct Dims {
         return halton_dim(*sc, idx, dim++);
     }
 };
+// The same dimension counter reading the LDS-staged tables (k_shade).
+struct DimsL {
+    const DevScene* sc;
+    const HalLds* hl;
+    uint32_t idx;
+    int dim;
+    bool overflow;
+    __device__ __forceinline__ float get1() {
+        if (dim >= sc->max_dim) { overflow = true; ++dim; return 0.5f; }
+        return halton_dim(*sc, *hl, idx, dim++);
+    }
+};
 
 __device__ __forceinline__ S3 load_s3(const float* a, uint32_t n, uint32_t slot) {
     return s3(a[slot], a[n + slot], a[2 * n + slot]);
@@ -739,13 +751,14 @@ __device__ __forceinline__ void store_s3(float* a, uint32_t n, uint32_t slot, S3
 template <int kFt>
 __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ray, int* lightOut) {
     int mat, light;
-    prim_info<Ft<kFt>::sph>(sc, prim, &mat, &light);
+    const PrimRec rec = prim_rec(sc, prim);
+    prim_info<Ft<kFt>::sph>(sc, rec, &mat, &light);
     *lightOut = light;
     if (light < 0) return s3(0.f);
     const DevLight& l = sc.lights[PT_IDX(light, sc.n_lights)];
     if (l.two_sided) return l.L;
     SurfHit si;
-    if (!surface_at<Ft<kFt>::sph>(sc, prim, ray, &si)) return s3(0.f);
+    if (!surface_at<Ft<kFt>::sph>(sc, prim, rec, ray, &si)) return s3(0.f);
     return area_L(l, si.n, -ray.d);
 }
 
@@ -1031,7 +1044,7 @@ struct PathPre {
     S3 L, beta;
     Ray ray;
     NeeIn nee;
-    float4 r0, r1;  // the hit primitive's record words 0-1 (loaded once `hit` is in)
+    PrimRec rec;  // the hit primitive's record (loaded once `hit` is in)
 };
 // Two stages: the head (state word, payload flags, hits) two paths ahead, the
 // body one path ahead and only what the head says this step will read.
@@ -1053,18 +1066,16 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
     if (p->st & kStNee) p->nee = nee_load(ps, slot, p->nfl, p->hitA);
 }
 __device__ __forceinline__ void path_prefetch_prim(const DevScene& sc, PathPre* p) {
-    if ((p->st & kStCont) && p->hit >= 0) {
-        p->r0 = sc.prims[3 * PT_IDX(p->hit, sc.n_prims)];
-        p->r1 = sc.prims[3 * PT_IDX(p->hit, sc.n_prims) + 1];
-    }
+    if ((p->st & kStCont) && p->hit >= 0) p->rec = prim_rec(sc, p->hit);
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
 // k_shade roofline): the SoA fields the reference's Li loop carries from one
 // vertex to the next, plus the queue entries (scene tables are not counted).
 template <int kFt>
-__device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& ps, uint32_t slot, const PathPre& pre,
-                                           uint32_t* rays, uint32_t* nrays, bool* keep, bool* overflow, uint32_t* ab) {
+__device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl, const DevPaths& ps, uint32_t slot,
+                                           const PathPre& pre, uint32_t* rays, uint32_t* nrays, bool* keep,
+                                           bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     *nrays = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
@@ -1096,9 +1107,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
         S3 beta = pre.beta;
         *ab += 24 + 4 + 12;
         SurfHit si;
-        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, pre.r0, pre.r1, ray, &si);
+        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, pre.rec, ray, &si);
         int mat = -1, light = -1;
-        if (found) prim_info<Ft<kFt>::sph>(sc, pre.r0, pre.r1, &mat, &light);
+        if (found) prim_info<Ft<kFt>::sph>(sc, pre.rec, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[PT_IDX(light, sc.n_lights)], si.n, -ray.d) : s3(0.f));
             else if (Ft<kFt>::inf)
@@ -1114,7 +1125,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const DevPaths& p
                 st |= kStCont;
                 rays[(*nrays)++] = slot << 2 | kRayCont;
             } else {
-                Dims dm{&sc, pre.hidx, (int)(st & kStDimMask), false};
+                DimsL dm{&sc, &hl, pre.hidx, (int)(st & kStDimMask), false};
                 *ab += 4;
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
@@ -1211,6 +1222,8 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     const uint32_t n = *pq_count;
     bool overflow = false;
     PT_WAVEQ(wq);
+    extern __shared__ uint4 pt_shade_lds[];
+    const HalLds hl = stage_halton(sc, pt_shade_lds);
     uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     const uint32_t stride = gridDim.x * blockDim.x;
     // software pipeline over the grid-stride iterations: while this path is
@@ -1242,7 +1255,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
         uint32_t rays[3];
         uint32_t nrays = 0;
         bool keep = false;
-        if (i < n) shade_path<kFt>(sc, ps, slot, pre, rays, &nrays, &keep, &overflow, &ab);
+        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, rays, &nrays, &keep, &overflow, &ab);
         if (i + stride < n) path_prefetch_prim(sc, &nxt);  // nxt.hit has arrived by now
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;

@@ -261,6 +261,7 @@ struct pt_scene {
     size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (8 M for the 60-bin hero state)
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
+    size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
     int shade_variant = 0;       // 0: compiler register budget (no scratch), 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
@@ -664,12 +665,17 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
         const pt_prim& p = d->prims[s->host_prim_order[i]];
         uint32_t flags = 0;
         V3 a = v3(0, 0, 0), b = a, c = a;
+        int pmat = 0, plight = -1;
         if (p.kind == PT_PRIM_AAPLANE) {
             flags = kPrimPlane;
+            pmat = d->planes[p.index].material; plight = d->planes[p.index].area_light;
         } else if (p.kind == PT_PRIM_SPHERE) {
             flags = kPrimSphere;
+            pmat = d->spheres[p.index].material; plight = d->spheres[p.index].area_light;
         } else {
             const pt_triangle& t = d->triangles[p.index];
+            pmat = t.material; plight = t.area_light;
+            flags |= (t.flags & 31u) << kPrimTriShift;
             a = Pv(t.v[0]); b = Pv(t.v[1]); c = Pv(t.v[2]);
             // Would Triangle::Intersect reject every ray after the t test?
             // (triangle.cpp:297-318: degenerate dp/duv and zero geometric normal)
@@ -691,9 +697,12 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
                 if (len2(cross(c - a, b - a)) == 0) flags |= kPrimDegenerate;
             }
         }
-        prims[3 * i] = make_float4(a.x, a.y, a.z, __builtin_bit_cast(float, flags));
         prims[3 * i + 1] = make_float4(b.x, b.y, b.z, __builtin_bit_cast(float, p.index));
-        prims[3 * i + 2] = make_float4(c.x, c.y, c.z, 0.f);
+        uint32_t info = 0;
+        if (prim_info_fits(pmat, plight)) info = prim_info_word(pmat, plight);
+        else flags |= kPrimInfoTable;
+        prims[3 * i] = make_float4(a.x, a.y, a.z, __builtin_bit_cast(float, flags));
+        prims[3 * i + 2] = make_float4(c.x, c.y, c.z, __builtin_bit_cast(float, info));
     }
     s->nodes.upload(nodes);
     s->prims.upload(prims);
@@ -955,6 +964,19 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     ds.divs = s->divs.p;
     ds.perm_c0 = s->perm_c0.p;
     ds.max_dim = max_dim;
+    // the shading kernel stages the leading dimensions' tables in LDS: as many as fit kHalLdsMax
+    // (16 + 4 bytes per dimension + 2 per permutation entry); PT_HAL_LDS=0 disables
+    {
+        int D = 0;
+        const char* e = std::getenv("PT_HAL_LDS");
+        if (!(e && e[0] == '0'))
+            while (D < max_dim && D < (int)ht.prime_sums.size() - 1 &&
+                   (size_t)20 * (D + 1) + 2 * (size_t)ht.prime_sums[D + 1] <= kHalLdsMax && ht.prime_sums[D + 1] < 65536)
+                ++D;
+        ds.hal_lds_dims = D;
+        ds.hal_lds_perm = D > 0 ? ht.prime_sums[D] : 0;
+        s->hal_lds_bytes = D > 0 ? (size_t)20 * D + 2 * (size_t)ds.hal_lds_perm : 0;
+    }
     ds.hal_exp0 = exps[0];
     ds.hal_scale1 = (uint32_t)scales[1];
     ds.div_scale1 = make_div_magic((uint32_t)scales[1]);
@@ -1230,8 +1252,8 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 } else {
                     const ShadeKernel kshade =
                         direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
-                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), 0, st, s->dev, ps, pq_in, counts + 1,
-                                       rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
+                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
+                                       pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(es.second, st));
