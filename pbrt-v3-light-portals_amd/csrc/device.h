@@ -122,6 +122,7 @@ struct DevScene {
     int max_dim;
     int hal_lds_dims;       // leading dimensions whose tables the shading kernel stages in LDS (0: none)
     int hal_lds_perm;       // their permutation entries (prime_sums[hal_lds_dims])
+    int hal_lds_bytes;      // bytes of the staged Halton tables (16-byte aligned): the scene tables follow
     int hal_exp0;
     uint32_t hal_scale1;
     DivMagic div_scale1;
@@ -140,6 +141,28 @@ struct DevScene {
     int dl_frames;          // recursion stack frames allocated per sample
     int wvl_dim;            // Halton dimension of CameraSample::wvl (5, or arrayEndDim with arrays)
 };
+
+// Scene tables the shading kernel stages in LDS next to the Halton tables
+// (k_shade_tab, small scenes): byte offsets from the start of the table
+// region, each 16-byte aligned, in this order.  The host sizes the region with
+// the same function.
+struct TabLayout {
+    uint32_t prims, mats, lights, planes, pplanes, lfunc, lcdf, end;
+};
+__host__ __device__ inline uint32_t tab_align16(uint32_t b) { return (b + 15u) & ~15u; }
+__host__ __device__ inline TabLayout tab_layout(int n_prims, int n_mats, int n_lights, int n_planes, int n_pplanes) {
+    TabLayout t;
+    uint32_t o = 0;
+    t.prims = o; o = tab_align16(o + 48u * (uint32_t)n_prims);
+    t.mats = o; o = tab_align16(o + (uint32_t)sizeof(pt_material) * (uint32_t)n_mats);
+    t.lights = o; o = tab_align16(o + (uint32_t)sizeof(DevLight) * (uint32_t)n_lights);
+    t.planes = o; o = tab_align16(o + (uint32_t)sizeof(DevPlane) * (uint32_t)n_planes);
+    t.pplanes = o; o = tab_align16(o + (uint32_t)sizeof(DevPlane) * (uint32_t)n_pplanes);
+    t.lfunc = o; o = tab_align16(o + 4u * (uint32_t)(n_lights > 0 ? n_lights : 1));
+    t.lcdf = o; o = tab_align16(o + 4u * (uint32_t)(n_lights + 2));
+    t.end = o;
+    return t;
+}
 
 // Per-path SoA state for one batch of nslots camera samples.
 struct DevPaths {

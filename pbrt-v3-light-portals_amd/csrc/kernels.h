@@ -23,7 +23,8 @@ constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
 constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h
 constexpr int kLdsSceneMax = 16384;  // bytes of BVH nodes + prim records staged in LDS by k_trace<true>
-constexpr size_t kHalLdsMax = 32768;  // bytes of Halton tables staged in LDS by k_shade (DevScene::hal_lds_dims)
+constexpr size_t kTabLdsMax = 8192;   // bytes of scene tables k_shade_tab stages in LDS after the Halton tables
+constexpr size_t kHalLdsMax = 28672;  // bytes of Halton tables staged in LDS by k_shade (DevScene::hal_lds_dims)
 
 // HaltonSampler constants for the per-pixel offset (halton.cpp:65-93)
 struct HaltonPixelConsts {

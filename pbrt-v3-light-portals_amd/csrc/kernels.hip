@@ -1214,8 +1214,41 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
     *ab += 4 * (*nrays + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
 
-template <int kFt>
-__device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& ps, const uint32_t* __restrict__ pq,
+// Copy n 4-byte words global -> LDS, the whole block.
+__device__ __forceinline__ void lds_copy_words(void* dst, const void* src, uint32_t bytes) {
+    uint32_t* d = (uint32_t*)dst;
+    const uint32_t* g = (const uint32_t*)src;
+    for (uint32_t i = threadIdx.x; i < bytes / 4u; i += blockDim.x) d[i] = g[i];
+}
+// k_shade_tab: the scene tables a path step reads (primitive records,
+// materials, lights and their planes, portal planes, the light distribution)
+// copied into LDS after the Halton tables, and a scene view whose table
+// pointers address the LDS copies -- the step's chains of dependent
+// scene-table loads then wait on LDS (lgkmcnt), not behind the path-state
+// loads and stores in flight (vmcnt counts in issue order).
+__device__ __forceinline__ DevScene stage_tables(const DevScene& sc, uint4* lds) {
+    const TabLayout t = tab_layout(sc.n_prims, sc.n_mats, sc.n_lights, sc.n_planes, sc.n_pplanes);
+    char* base = (char*)lds + sc.hal_lds_bytes;
+    lds_copy_words(base + t.prims, sc.prims, 48u * (uint32_t)sc.n_prims);
+    lds_copy_words(base + t.mats, sc.mats, (uint32_t)sizeof(pt_material) * (uint32_t)sc.n_mats);
+    lds_copy_words(base + t.lights, sc.lights, (uint32_t)sizeof(DevLight) * (uint32_t)sc.n_lights);
+    lds_copy_words(base + t.planes, sc.planes, (uint32_t)sizeof(DevPlane) * (uint32_t)sc.n_planes);
+    lds_copy_words(base + t.pplanes, sc.portal_planes, (uint32_t)sizeof(DevPlane) * (uint32_t)sc.n_pplanes);
+    lds_copy_words(base + t.lfunc, sc.ldist_func, 4u * (uint32_t)sc.n_lights);
+    lds_copy_words(base + t.lcdf, sc.ldist_cdf, 4u * (uint32_t)(sc.n_lights + 1));
+    DevScene v = sc;
+    v.prims = (const float4*)(base + t.prims);
+    v.mats = (const pt_material*)(base + t.mats);
+    v.lights = (const DevLight*)(base + t.lights);
+    v.planes = (const DevPlane*)(base + t.planes);
+    v.portal_planes = (const DevPlane*)(base + t.pplanes);
+    v.ldist_func = (const float*)(base + t.lfunc);
+    v.ldist_cdf = (const float*)(base + t.lcdf);
+    return v;
+}
+
+template <int kFt, bool kTab>
+__device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
                                             DevStats* stats) {
@@ -1223,7 +1256,8 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc, const DevPaths& 
     bool overflow = false;
     PT_WAVEQ(wq);
     extern __shared__ uint4 pt_shade_lds[];
-    const HalLds hl = stage_halton(sc, pt_shade_lds);
+    const DevScene sc = kTab ? stage_tables(sc0, pt_shade_lds) : sc0;
+    const HalLds hl = stage_halton(sc0, pt_shade_lds);  // its __syncthreads also covers the tables
     uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     const uint32_t stride = gridDim.x * blockDim.x;
     // software pipeline over the grid-stride iterations: while this path is
@@ -1563,7 +1597,20 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps,
                                                        uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, false>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+#else
+;
+#endif
+// The scene tables in LDS (stage_tables): scenes whose tables fit kTabLdsMax.
+template <int kFt>
+__global__ __launch_bounds__(kShadeBlock) void k_shade_tab(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
+                                                           const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+                                                           uint32_t* rq_out_count, uint32_t* pq_out,
+                                                           uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
+    shade_batch<kFt, true>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;
@@ -1574,18 +1621,7 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
-}
-#else
-;
-#endif
-template <int kFt>
-__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_w4(
-    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
-    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
-#ifdef PT_TU_SHADE
-{
-    shade_batch<kFt>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, false>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;

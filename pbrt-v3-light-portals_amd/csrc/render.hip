@@ -262,6 +262,7 @@ struct pt_scene {
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
+    bool shade_tab = false;      // k_shade_tab: the scene tables staged in LDS as well (small scenes)
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
     int shade_variant = 0;       // 0: compiler register budget (no scratch), 3/4: forced waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
@@ -320,7 +321,7 @@ template <int kFt>
 static ShadeKernel shade_kernel_ft(int variant) {
     switch (variant) {
         case 3: return k_shade_w3<kFt>;
-        case 4: return k_shade_w4<kFt>;
+        case 5: return k_shade_tab<kFt>;
         default: return k_shade<kFt>;
     }
 }
@@ -975,7 +976,13 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
                 ++D;
         ds.hal_lds_dims = D;
         ds.hal_lds_perm = D > 0 ? ht.prime_sums[D] : 0;
-        s->hal_lds_bytes = D > 0 ? (size_t)20 * D + 2 * (size_t)ds.hal_lds_perm : 0;
+        ds.hal_lds_bytes = (int)tab_align16(D > 0 ? (uint32_t)(20 * D + 2 * ds.hal_lds_perm) : 0u);
+        s->hal_lds_bytes = (size_t)ds.hal_lds_bytes;
+        // k_shade_tab: the scene tables after them, when they fit kTabLdsMax (PT_SHADE_TAB=0 disables)
+        const TabLayout tl = tab_layout((int)s->host_prim_order.size(), d->n_materials, nl, d->n_planes, d->n_portals);
+        const char* et = std::getenv("PT_SHADE_TAB");
+        s->shade_tab = tl.end <= kTabLdsMax && !(et && et[0] == '0');
+        if (s->shade_tab) s->hal_lds_bytes += tl.end;
     }
     ds.hal_exp0 = exps[0];
     ds.hal_scale1 = (uint32_t)scales[1];
@@ -1251,7 +1258,8 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                                        counts + 2, pq_out, counts + 3, w.stats.p);
                 } else {
                     const ShadeKernel kshade =
-                        direct ? k_shade_dl<kFtAll> : shade_kernel(s->shade_variant, s->features);
+                        direct ? k_shade_dl<kFtAll>
+                               : shade_kernel(s->shade_tab && s->shade_variant == 0 ? 5 : s->shade_variant, s->features);
                     hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
                                        pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }

@@ -7,9 +7,9 @@
 namespace pt {
 #define PT_ARGS DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, DevStats*
 #define PT_SHADE_FT(F)                                \
-    template __global__ void k_shade<F>(PT_ARGS);    \
-    template __global__ void k_shade_w3<F>(PT_ARGS); \
-    template __global__ void k_shade_w4<F>(PT_ARGS);
+    template __global__ void k_shade<F>(PT_ARGS);     \
+    template __global__ void k_shade_tab<F>(PT_ARGS); \
+    template __global__ void k_shade_w3<F>(PT_ARGS);
 #if !defined(PT_FT) || PT_FT == 0
 PT_SHADE_FT(0)
 #endif
