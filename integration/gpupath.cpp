@@ -10,11 +10,20 @@
 #include "core/error.h"
 #include "core/film.h"
 #include "core/primitive.h"
+#include "core/microfacet.h"
 #include "lights/diffuse.h"
+#include "lights/infinite.h"
+#include "lights/point.h"
 #include "lights/portal_arealight.h"
+#include "materials/dispersive_glass.h"
+#include "materials/glass.h"
 #include "materials/matte.h"
+#include "materials/metal.h"
+#include "materials/mirror.h"
+#include "materials/plastic.h"
 #include "portals/aaportal.h"
 #include "shapes/plane.h"
+#include "shapes/sphere.h"
 #include "shapes/triangle.h"
 #include "textures/constant.h"
 
@@ -26,6 +35,23 @@ static void to_pt(const Transform& t, pt_transform* out) {
             out->m[4 * i + j] = t.GetMatrix().m[i][j];
             out->minv[4 * i + j] = t.GetInverseMatrix().m[i][j];
         }
+}
+
+// The value of a ConstantTexture (false for any other texture); a null
+// texture keeps *out.
+template <typename T>
+static bool constant_value(const std::shared_ptr<Texture<T>>& t, T* out) {
+    if (!t) return true;
+    const auto* c = dynamic_cast<const ConstantTexture<T>*>(t.get());
+    if (!c) return false;
+    *out = c->Evaluate(SurfaceInteraction());
+    return true;
+}
+// A microfacet material's alpha: RoughnessToAlpha when it remaps, then the
+// TrowbridgeReitzDistribution ctor's floor (microfacet.h:109-132).
+static Float tr_alpha(Float rough, bool remap) {
+    if (remap) rough = TrowbridgeReitzDistribution::RoughnessToAlpha(rough);
+    return std::max(Float(0.001), rough);
 }
 
 static uint32_t shape_flags(const Shape& s) {
@@ -47,7 +73,7 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
     for (size_t i = 0; i < scene.lights.size(); ++i) lightIndex[scene.lights[i].get()] = (int)i;
     std::unordered_map<const Material*, int> materialIndex;
     std::unordered_map<const TriangleMesh*, int> meshBase;
-    std::unordered_map<const Shape*, int> triIndex, planeIndex;
+    std::unordered_map<const Shape*, int> triIndex, planeIndex, sphereIndex;
     bool anyN = false, anyS = false, anyUV = false;
     for (const auto& p : bvh->GetPrimitives()) {
         const auto* gp = dynamic_cast<const GeometricPrimitive*>(p.get());
@@ -73,8 +99,85 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
             pm.kind = PT_MAT_MATTE;
             kd->Evaluate(SurfaceInteraction()).ToRGB(pm.kd);
             pm.sigma = sg->Evaluate(SurfaceInteraction());
+        } else if (const auto* me = dynamic_cast<const MetalMaterial*>(m)) {
+            // MetalMaterial::ComputeScatteringFunctions (metal.cpp:58-79)
+            Spectrum eta, k;
+            Float rough = 0, ur = 0, vr = 0;
+            if (!constant_value(me->GetEta(), &eta) || !constant_value(me->GetK(), &k) ||
+                !constant_value(me->GetRoughness(), &rough) || !constant_value(me->GetURoughness(), &ur) ||
+                !constant_value(me->GetVRoughness(), &vr)) {
+                *err = "gpupath: metal with non-constant textures";
+                return false;
+            }
+            if (!me->GetURoughness()) ur = rough;
+            if (!me->GetVRoughness()) vr = rough;
+            pm.kind = PT_MAT_METAL;
+            eta.ToRGB(pm.eta);
+            k.ToRGB(pm.k);
+            pm.alpha[0] = tr_alpha(ur, me->RemapRoughness());
+            pm.alpha[1] = tr_alpha(vr, me->RemapRoughness());
+        } else if (const auto* gm = dynamic_cast<const GlassMaterial*>(m)) {
+            // GlassMaterial::ComputeScatteringFunctions (glass.cpp:45-83)
+            Spectrum kr(1.f), kt(1.f);
+            Float ur = 0, vr = 0, eta = 1.5f;
+            if (!constant_value(gm->GetKr(), &kr) || !constant_value(gm->GetKt(), &kt) ||
+                !constant_value(gm->GetURoughness(), &ur) || !constant_value(gm->GetVRoughness(), &vr) ||
+                !constant_value(gm->GetIndex(), &eta)) {
+                *err = "gpupath: glass with non-constant textures";
+                return false;
+            }
+            pm.kind = PT_MAT_GLASS;
+            kr.ToRGB(pm.kr);
+            kt.ToRGB(pm.kt);
+            pm.ior = eta;
+            pm.specular = (ur == 0 && vr == 0) ? 1 : 0;  // isSpecular before the remap (glass.cpp:56)
+            pm.alpha[0] = tr_alpha(ur, gm->RemapRoughness());
+            pm.alpha[1] = tr_alpha(vr, gm->RemapRoughness());
+        } else if (const auto* dg = dynamic_cast<const DispersiveGlassMaterial*>(m)) {
+            // DispersiveGlassMaterial::ComputeScatteringFunctions (dispersive_glass.cpp:48-123):
+            // eta by Cauchy from wvls[0] between indexMin and indexMax
+            Spectrum kr(1.f), kt(1.f);
+            Float ur = 0, vr = 0, etaMin = 1.5f, etaMax = 1.5f;
+            if (!constant_value(dg->GetKr(), &kr) || !constant_value(dg->GetKt(), &kt) ||
+                !constant_value(dg->GetURoughness(), &ur) || !constant_value(dg->GetVRoughness(), &vr) ||
+                !constant_value(dg->GetIndexMin(), &etaMin) || !constant_value(dg->GetIndexMax(), &etaMax)) {
+                *err = "gpupath: dispersive glass with non-constant textures";
+                return false;
+            }
+            pm.kind = PT_MAT_DISPERSIVE_GLASS;
+            kr.ToRGB(pm.kr);
+            kt.ToRGB(pm.kt);
+            pm.ior_min = etaMin;
+            pm.ior_max = etaMax;
+            pm.specular = (ur == 0 && vr == 0) ? 1 : 0;
+            if (dg->RemapRoughness() && !pm.specular) {  // remapped once per wavelength BSDF, cumulatively (:91-95)
+                *err = "gpupath: rough dispersive glass with remaproughness is not flattened";
+                return false;
+            }
+            pm.alpha[0] = tr_alpha(ur, dg->RemapRoughness());
+            pm.alpha[1] = tr_alpha(vr, dg->RemapRoughness());
+        } else if (const auto* mr = dynamic_cast<const MirrorMaterial*>(m)) {
+            Spectrum kr(0.9f);  // mirror.cpp:44-52
+            if (!constant_value(mr->GetKr(), &kr)) {
+                *err = "gpupath: mirror with a non-constant Kr";
+                return false;
+            }
+            pm.kind = PT_MAT_MIRROR;
+            kr.ToRGB(pm.kr);
+        } else if (const auto* pl = dynamic_cast<const PlasticMaterial*>(m)) {
+            Spectrum kd(0.25f), ks(0.25f);  // plastic.cpp:45-70
+            Float rough = 0.1f;
+            if (!constant_value(pl->GetKd(), &kd) || !constant_value(pl->GetKs(), &ks) ||
+                !constant_value(pl->GetRoughness(), &rough)) {
+                *err = "gpupath: plastic with non-constant textures";
+                return false;
+            }
+            pm.kind = PT_MAT_PLASTIC;
+            kd.ToRGB(pm.kd);
+            ks.ToRGB(pm.ks);
+            pm.alpha[0] = pm.alpha[1] = tr_alpha(rough, pl->RemapRoughness());
         } else {
-            *err = "gpupath: only MatteMaterial is flattened from scene objects (use pt_load_pbrt for the rest)";
+            *err = "gpupath: unsupported material (matte, metal, glass, dispersive glass, mirror, plastic)";
             return false;
         }
         *out = (int)f->materials.size();
@@ -137,8 +240,22 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
             planeIndex[a] = (int)f->planes.size();
             f->prims.push_back({PT_PRIM_AAPLANE, (int32_t)f->planes.size()});
             f->planes.push_back(pl);
+        } else if (const auto* sp = dynamic_cast<const Sphere*>(sh)) {
+            pt_sphere ps;  // CreateSphereShape's parameters (sphere.cpp:381-391)
+            std::memset(&ps, 0, sizeof ps);
+            ps.radius = sp->Radius();
+            ps.zmin = sp->ZMin();
+            ps.zmax = sp->ZMax();
+            ps.phimax = sp->PhiMaxDegrees();
+            ps.material = mi;
+            ps.area_light = area_light(gp->GetAreaLight());
+            ps.flags = shape_flags(*sp);
+            to_pt(*sp->ObjectToWorld, &ps.object_to_world);
+            sphereIndex[sp] = (int)f->spheres.size();
+            f->prims.push_back({PT_PRIM_SPHERE, (int32_t)f->spheres.size()});
+            f->spheres.push_back(ps);
         } else
-            return fail("gpupath: unsupported shape (triangles and aaplanes are flattened from scene objects)");
+            return fail("gpupath: unsupported shape (triangles, aaplanes and spheres are flattened)");
     }
 
     // ---- lights ----
@@ -169,14 +286,34 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
             pl->GetLemit().ToRGB(l.L);
             l.two_sided = pl->TwoSided() ? 1 : 0;
         } else if (const auto* dl = dynamic_cast<const DiffuseAreaLight*>(lp.get())) {
-            l.kind = PT_LIGHT_DIFFUSE_AREA;
-            auto it = triIndex.find(dl->GetShape());
-            if (it == triIndex.end()) return fail("gpupath: diffuse area light on a shape other than a triangle");
-            l.shape = it->second;
+            // on a triangle, a sphere or an aaplane (creeper.pbrt:38-49)
+            const Shape* shp = dl->GetShape();
+            if (triIndex.count(shp)) { l.kind = PT_LIGHT_DIFFUSE_AREA; l.shape = triIndex.at(shp); }
+            else if (sphereIndex.count(shp)) { l.kind = PT_LIGHT_DIFFUSE_SPHERE; l.shape = sphereIndex.at(shp); }
+            else if (planeIndex.count(shp)) { l.kind = PT_LIGHT_DIFFUSE_PLANE; l.shape = planeIndex.at(shp); }
+            else return fail("gpupath: diffuse area light whose shape is not in the aggregate");
             dl->GetLemit().ToRGB(l.L);
             l.two_sided = dl->TwoSided() ? 1 : 0;
+        } else if (const auto* pt = dynamic_cast<const PointLight*>(lp.get())) {
+            // PointLight (point.cpp:41-49): pLight; the renderer takes it as
+            // LightToWorld(0, 0, 0), so a translation to pLight reproduces it exactly
+            l.kind = PT_LIGHT_POINT;
+            l.shape = -1;
+            pt->GetIntensity().ToRGB(l.L);
+            Matrix4x4 m, mi;
+            const Point3f& p = pt->GetPosition();
+            m.m[0][3] = p.x; m.m[1][3] = p.y; m.m[2][3] = p.z;
+            mi.m[0][3] = -p.x; mi.m[1][3] = -p.y; mi.m[2][3] = -p.z;
+            to_pt(Transform(m, mi), &l.light_to_world);
+        } else if (const auto* il = dynamic_cast<const InfiniteAreaLight*>(lp.get())) {
+            const Spectrum* Lc = il->ConstantRadiance();  // infinite.cpp:43-61, a 1x1 Lmap
+            if (!Lc) return fail("gpupath: infinite light with an image map (only a constant radiance is flattened)");
+            l.kind = PT_LIGHT_INFINITE;
+            l.shape = -1;
+            Lc->ToRGB(l.L);
+            to_pt(il->GetLightToWorld(), &l.light_to_world);
         } else
-            return fail("gpupath: unsupported light (diffuse area and portal lights are flattened)");
+            return fail("gpupath: unsupported light (diffuse area, portal, point and constant infinite lights)");
         f->lights.push_back(l);
     }
 
@@ -204,6 +341,8 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
     d.lights = f->lights.data();
     d.n_portals = (int32_t)f->portals.size();
     d.portals = f->portals.data();
+    d.n_spheres = (int32_t)f->spheres.size();
+    d.spheres = f->spheres.data();
     d.bvh_max_prims = 4;
     d.camera = settings.camera;
     d.film = settings.film;
@@ -238,16 +377,70 @@ void GpuPathIntegrator::Render(const Scene& scene) {
     pt_scene_destroy(s);
 }
 
+static GpuRenderSettings common_settings(const ParamSet& params, const ParamSet& cameraParams,
+                                         const ParamSet& filmParams, const std::string& filterName,
+                                         const ParamSet& filterParams, const ParamSet& samplerParams,
+                                         const Transform& cameraToWorld, const Camera& camera);
+static std::vector<int> gpu_list(const ParamSet& params) {
+    std::vector<int> gpus{0};
+    int ng = 0;
+    if (const int* g = params.FindInt("gpus", &ng))
+        if (ng > 0) gpus.assign(g, g + ng);
+    return gpus;
+}
+static void pixel_bounds(const ParamSet& params, pt_integrator_desc* d) {
+    int np = 0;
+    if (const int* pb = params.FindInt("pixelbounds", &np))
+        if (np == 4) {
+            d->has_pixel_bounds = 1;
+            for (int i = 0; i < 4; ++i) d->pixel_bounds[i] = pb[i];
+        }
+}
+
 GpuPathIntegrator* CreateGpuPathIntegrator(const ParamSet& params, const ParamSet& cameraParams,
                                            const ParamSet& filmParams, const std::string& filterName,
                                            const ParamSet& filterParams, const ParamSet& samplerParams,
                                            const Transform& cameraToWorld, std::shared_ptr<const Camera> camera) {
+    GpuRenderSettings s = common_settings(params, cameraParams, filmParams, filterName, filterParams, samplerParams,
+                                          cameraToWorld, *camera);
+    // PathIntegrator (path.cpp:191-214; the fork's default strategy "uniform", path.cpp:210-211)
+    s.integrator.kind = PT_INTEGRATOR_PATH;
+    s.integrator.max_depth = params.FindOneInt("maxdepth", 5);
+    s.integrator.rr_threshold = params.FindOneFloat("rrthreshold", 1.f);
+    const std::string ls = params.FindOneString("lightsamplestrategy", "uniform");
+    s.integrator.light_strategy = ls == "power" ? PT_LIGHTS_POWER : PT_LIGHTS_UNIFORM;
+    pixel_bounds(params, &s.integrator);
+    return new GpuPathIntegrator(std::move(s), std::move(camera), gpu_list(params));
+}
+
+GpuPathIntegrator* CreateGpuDirectLightingIntegrator(const ParamSet& params, const ParamSet& cameraParams,
+                                                     const ParamSet& filmParams, const std::string& filterName,
+                                                     const ParamSet& filterParams, const ParamSet& samplerParams,
+                                                     const Transform& cameraToWorld,
+                                                     std::shared_ptr<const Camera> camera) {
+    GpuRenderSettings s = common_settings(params, cameraParams, filmParams, filterName, filterParams, samplerParams,
+                                          cameraToWorld, *camera);
+    // DirectLightingIntegrator (directlighting.cpp:86-118): "strategy" all (default) | one
+    s.integrator.kind = PT_INTEGRATOR_DIRECT;
+    s.integrator.max_depth = params.FindOneInt("maxdepth", 5);
+    s.integrator.rr_threshold = 1.f;
+    s.integrator.light_strategy = PT_LIGHTS_UNIFORM;
+    const std::string st = params.FindOneString("strategy", "all");
+    s.integrator.direct_strategy = st == "one" ? PT_DIRECT_ONE : PT_DIRECT_ALL;
+    pixel_bounds(params, &s.integrator);
+    return new GpuPathIntegrator(std::move(s), std::move(camera), gpu_list(params));
+}
+
+static GpuRenderSettings common_settings(const ParamSet& params, const ParamSet& cameraParams,
+                                         const ParamSet& filmParams, const std::string& filterName,
+                                         const ParamSet& filterParams, const ParamSet& samplerParams,
+                                         const Transform& cameraToWorld, const Camera& camera) {
     GpuRenderSettings s;
     std::memset(&s.camera, 0, sizeof s.camera);
     std::memset(&s.film, 0, sizeof s.film);
     std::memset(&s.sampler, 0, sizeof s.sampler);
     std::memset(&s.integrator, 0, sizeof s.integrator);
-    const Film* film = camera->film;
+    const Film* film = camera.film;
     // Film (film.cpp:213-252): resolution, crop window, scale, luminance clamp
     s.film.xres = film->fullResolution.x;
     s.film.yres = film->fullResolution.y;
@@ -304,23 +497,8 @@ GpuPathIntegrator* CreateGpuPathIntegrator(const ParamSet& params, const ParamSe
     // HaltonSampler (halton.cpp:133-139)
     s.sampler.spp = samplerParams.FindOneInt("pixelsamples", 16);
     s.sampler.sample_pixel_center = samplerParams.FindOneBool("samplepixelcenter", false) ? 1 : 0;
-    // PathIntegrator (path.cpp:191-214; the fork's default strategy "uniform", path.cpp:210-211)
-    s.integrator.kind = PT_INTEGRATOR_PATH;
-    s.integrator.max_depth = params.FindOneInt("maxdepth", 5);
-    s.integrator.rr_threshold = params.FindOneFloat("rrthreshold", 1.f);
-    const std::string ls = params.FindOneString("lightsamplestrategy", "uniform");
-    s.integrator.light_strategy = ls == "power" ? PT_LIGHTS_POWER : PT_LIGHTS_UNIFORM;
-    int np = 0;
-    if (const int* pb = params.FindInt("pixelbounds", &np))
-        if (np == 4) {
-            s.integrator.has_pixel_bounds = 1;
-            for (int i = 0; i < 4; ++i) s.integrator.pixel_bounds[i] = pb[i];
-        }
-    std::vector<int> gpus{0};
-    int ng = 0;
-    if (const int* g = params.FindInt("gpus", &ng))
-        if (ng > 0) gpus.assign(g, g + ng);
-    return new GpuPathIntegrator(std::move(s), std::move(camera), std::move(gpus));
+    (void)params;
+    return s;
 }
 
 }  // namespace pbrt

@@ -10,10 +10,16 @@
 //         integrator = CreateGpuPathIntegrator(IntegratorParams, CameraParams, FilmParams, FilterName,
 //                                              FilterParams, SamplerParams, CameraToWorld[0], camera);
 //
-// The integrator replaces PathIntegrator (src/integrators/path.cpp:64-214):
-// same "maxdepth" / "rrthreshold" / "lightsamplestrategy" / "pixelbounds"
-// parameters, the scene's Halton sampler and perspective camera, the Film's
-// filter, crop window and file name.
+//     else if (IntegratorName == "gpudirectlighting")
+//         integrator = CreateGpuDirectLightingIntegrator(IntegratorParams, CameraParams, FilmParams, FilterName,
+//                                                        FilterParams, SamplerParams, CameraToWorld[0], camera);
+//
+// "gpupath" replaces PathIntegrator (src/integrators/path.cpp:64-214): same
+// "maxdepth" / "rrthreshold" / "lightsamplestrategy" / "pixelbounds"
+// parameters; "gpudirectlighting" replaces DirectLightingIntegrator
+// (src/integrators/directlighting.cpp:86-118): "strategy" / "maxdepth" /
+// "pixelbounds".  Both use the scene's Halton sampler and perspective camera,
+// the Film's filter, crop window and file name.
 #ifndef PBRT_INTEGRATORS_GPUPATH_H
 #define PBRT_INTEGRATORS_GPUPATH_H
 
@@ -38,6 +44,7 @@ struct GpuFlatScene {
     std::vector<float> P, N, S, UV;
     std::vector<pt_triangle> triangles;
     std::vector<pt_aaplane> planes;
+    std::vector<pt_sphere> spheres;
     std::vector<pt_prim> prims;
     std::vector<pt_material> materials;
     std::vector<pt_light> lights;
@@ -57,9 +64,11 @@ struct GpuRenderSettings {
 };
 
 // Flatten `scene` (Scene::aggregate = a BVHAccel of GeometricPrimitives over
-// Triangle / AAPlaneShape shapes, MatteMaterial with constant textures,
-// DiffuseAreaLight / PortalArealight lights) into `out`.  Returns false and
-// fills `err` for anything the device path does not implement.
+// Triangle / AAPlaneShape / Sphere shapes; Matte, Metal, Glass, dispersive
+// glass, Mirror and Plastic materials with constant textures; DiffuseAreaLight on a triangle,
+// sphere or aaplane, PortalArealight, PointLight and a constant
+// InfiniteAreaLight) into `out`.  Returns false and fills `err` for anything
+// the device path does not implement.
 bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlatScene* out, std::string* err);
 
 class GpuPathIntegrator : public Integrator {
@@ -91,6 +100,14 @@ GpuPathIntegrator* CreateGpuPathIntegrator(const ParamSet& params, const ParamSe
                                            const ParamSet& filmParams, const std::string& filterName,
                                            const ParamSet& filterParams, const ParamSet& samplerParams,
                                            const Transform& cameraToWorld, std::shared_ptr<const Camera> camera);
+
+// CreateDirectLightingIntegrator's parameters (directlighting.cpp:86-118):
+// "strategy" all | one, "maxdepth" (default 5), "pixelbounds"; the rest as above.
+GpuPathIntegrator* CreateGpuDirectLightingIntegrator(const ParamSet& params, const ParamSet& cameraParams,
+                                                     const ParamSet& filmParams, const std::string& filterName,
+                                                     const ParamSet& filterParams, const ParamSet& samplerParams,
+                                                     const Transform& cameraToWorld,
+                                                     std::shared_ptr<const Camera> camera);
 
 }  // namespace pbrt
 

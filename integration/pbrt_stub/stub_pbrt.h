@@ -8,6 +8,7 @@
 // call them.
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -169,6 +170,120 @@ class MatteMaterial : public Material {
     std::shared_ptr<Texture<Float>> sigma, bumpMap;
 };
 
+// core/microfacet.h:105-133: the static remap of roughness to alpha
+class TrowbridgeReitzDistribution {
+  public:
+    static inline Float RoughnessToAlpha(Float roughness) {
+        roughness = std::max(roughness, (Float)1e-3);
+        Float x = std::log(roughness);
+        return 1.62142f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
+    }
+};
+
+// materials/metal.h:49-69
+class MetalMaterial : public Material {
+  public:
+    MetalMaterial(const std::shared_ptr<Texture<Spectrum>>& eta, const std::shared_ptr<Texture<Spectrum>>& k,
+                  const std::shared_ptr<Texture<Float>>& rough, const std::shared_ptr<Texture<Float>>& urough,
+                  const std::shared_ptr<Texture<Float>>& vrough, const std::shared_ptr<Texture<Float>>& bump,
+                  bool remapRoughness)
+        : eta(eta), k(k), roughness(rough), uRoughness(urough), vRoughness(vrough), bumpMap(bump),
+          remapRoughness(remapRoughness) {}
+    // PATCH: read access to the members (metal.h:65-68)
+    const std::shared_ptr<Texture<Spectrum>>& GetEta() const { return eta; }
+    const std::shared_ptr<Texture<Spectrum>>& GetK() const { return k; }
+    const std::shared_ptr<Texture<Float>>& GetRoughness() const { return roughness; }
+    const std::shared_ptr<Texture<Float>>& GetURoughness() const { return uRoughness; }
+    const std::shared_ptr<Texture<Float>>& GetVRoughness() const { return vRoughness; }
+    bool RemapRoughness() const { return remapRoughness; }
+  private:
+    std::shared_ptr<Texture<Spectrum>> eta, k;
+    std::shared_ptr<Texture<Float>> roughness, uRoughness, vRoughness;
+    std::shared_ptr<Texture<Float>> bumpMap;
+    bool remapRoughness;
+};
+
+// materials/glass.h:48-76
+class GlassMaterial : public Material {
+  public:
+    GlassMaterial(const std::shared_ptr<Texture<Spectrum>>& Kr, const std::shared_ptr<Texture<Spectrum>>& Kt,
+                  const std::shared_ptr<Texture<Float>>& uRoughness, const std::shared_ptr<Texture<Float>>& vRoughness,
+                  const std::shared_ptr<Texture<Float>>& index, const std::shared_ptr<Texture<Float>>& bumpMap,
+                  bool remapRoughness)
+        : Kr(Kr), Kt(Kt), uRoughness(uRoughness), vRoughness(vRoughness), index(index), bumpMap(bumpMap),
+          remapRoughness(remapRoughness) {}
+    // PATCH: read access to the members (glass.h:71-75)
+    const std::shared_ptr<Texture<Spectrum>>& GetKr() const { return Kr; }
+    const std::shared_ptr<Texture<Spectrum>>& GetKt() const { return Kt; }
+    const std::shared_ptr<Texture<Float>>& GetURoughness() const { return uRoughness; }
+    const std::shared_ptr<Texture<Float>>& GetVRoughness() const { return vRoughness; }
+    const std::shared_ptr<Texture<Float>>& GetIndex() const { return index; }
+    bool RemapRoughness() const { return remapRoughness; }
+  private:
+    std::shared_ptr<Texture<Spectrum>> Kr, Kt;
+    std::shared_ptr<Texture<Float>> uRoughness, vRoughness;
+    std::shared_ptr<Texture<Float>> index;
+    std::shared_ptr<Texture<Float>> bumpMap;
+    bool remapRoughness;
+};
+
+// materials/dispersive_glass.h:47-78 (the fork's Cauchy-dispersion glass)
+class DispersiveGlassMaterial : public Material {
+  public:
+    DispersiveGlassMaterial(const std::shared_ptr<Texture<Spectrum>>& Kr, const std::shared_ptr<Texture<Spectrum>>& Kt,
+                            const std::shared_ptr<Texture<Float>>& uRoughness,
+                            const std::shared_ptr<Texture<Float>>& vRoughness,
+                            const std::shared_ptr<Texture<Float>>& indexMin,
+                            const std::shared_ptr<Texture<Float>>& indexMax,
+                            const std::shared_ptr<Texture<Float>>& bumpMap, bool remapRoughness)
+        : Kr(Kr), Kt(Kt), uRoughness(uRoughness), vRoughness(vRoughness), indexMin(indexMin), indexMax(indexMax),
+          bumpMap(bumpMap), remapRoughness(remapRoughness) {}
+    // PATCH: read access to the members (dispersive_glass.h:70-76)
+    const std::shared_ptr<Texture<Spectrum>>& GetKr() const { return Kr; }
+    const std::shared_ptr<Texture<Spectrum>>& GetKt() const { return Kt; }
+    const std::shared_ptr<Texture<Float>>& GetURoughness() const { return uRoughness; }
+    const std::shared_ptr<Texture<Float>>& GetVRoughness() const { return vRoughness; }
+    const std::shared_ptr<Texture<Float>>& GetIndexMin() const { return indexMin; }
+    const std::shared_ptr<Texture<Float>>& GetIndexMax() const { return indexMax; }
+    bool RemapRoughness() const { return remapRoughness; }
+  private:
+    std::shared_ptr<Texture<Spectrum>> Kr, Kt;
+    std::shared_ptr<Texture<Float>> uRoughness, vRoughness;
+    std::shared_ptr<Texture<Float>> indexMin;
+    std::shared_ptr<Texture<Float>> indexMax;
+    std::shared_ptr<Texture<Float>> bumpMap;
+    bool remapRoughness;
+};
+
+// materials/mirror.h:48-64
+class MirrorMaterial : public Material {
+  public:
+    MirrorMaterial(const std::shared_ptr<Texture<Spectrum>>& r, const std::shared_ptr<Texture<Float>>& bump)
+        : Kr(r), bumpMap(bump) {}
+    const std::shared_ptr<Texture<Spectrum>>& GetKr() const { return Kr; }  // PATCH
+  private:
+    std::shared_ptr<Texture<Spectrum>> Kr;
+    std::shared_ptr<Texture<Float>> bumpMap;
+};
+
+// materials/plastic.h:48-70
+class PlasticMaterial : public Material {
+  public:
+    PlasticMaterial(const std::shared_ptr<Texture<Spectrum>>& Kd, const std::shared_ptr<Texture<Spectrum>>& Ks,
+                    const std::shared_ptr<Texture<Float>>& roughness, const std::shared_ptr<Texture<Float>>& bumpMap,
+                    bool remapRoughness)
+        : Kd(Kd), Ks(Ks), roughness(roughness), bumpMap(bumpMap), remapRoughness(remapRoughness) {}
+    // PATCH: read access to the members (plastic.h:67-69)
+    const std::shared_ptr<Texture<Spectrum>>& GetKd() const { return Kd; }
+    const std::shared_ptr<Texture<Spectrum>>& GetKs() const { return Ks; }
+    const std::shared_ptr<Texture<Float>>& GetRoughness() const { return roughness; }
+    bool RemapRoughness() const { return remapRoughness; }
+  private:
+    std::shared_ptr<Texture<Spectrum>> Kd, Ks;
+    std::shared_ptr<Texture<Float>> roughness, bumpMap;
+    const bool remapRoughness;
+};
+
 // core/shape.h (shape.h:52-88)
 class Shape {
   public:
@@ -228,6 +343,26 @@ class AAPlaneShape : public Shape {
     const int ax1;
 };
 
+// shapes/sphere.h:47-76
+class Sphere : public Shape {
+  public:
+    Sphere(const Transform* ObjectToWorld, const Transform* WorldToObject, bool reverseOrientation, Float radius,
+           Float zMin, Float zMax, Float phiMax)
+        : Shape(ObjectToWorld, WorldToObject, reverseOrientation), radius(radius),
+          zMin(std::min(std::max(std::min(zMin, zMax), -radius), radius)),
+          zMax(std::min(std::max(std::max(zMin, zMax), -radius), radius)), phiMaxDegrees(phiMax) {}
+    // PATCH: the creation parameters (the members keep phiMax in radians,
+    // Radians(Clamp(phiMax, 0, 360)), which does not round-trip exactly)
+    Float Radius() const { return radius; }
+    Float ZMin() const { return zMin; }
+    Float ZMax() const { return zMax; }
+    Float PhiMaxDegrees() const { return phiMaxDegrees; }
+  private:
+    const Float radius;
+    const Float zMin, zMax;
+    const Float phiMaxDegrees;
+};
+
 // portals/aaportal.h: the portal rectangle on the light's transforms (aaportal.cpp:8-12)
 class AAPortal {
   public:
@@ -262,6 +397,32 @@ class DiffuseAreaLight : public AreaLight {
     const Spectrum Lemit;
     std::shared_ptr<Shape> shape;
     const bool twoSided;
+};
+
+// lights/point.h:49-71: pLight = LightToWorld(Point3f(0, 0, 0)) (point.h:55)
+class PointLight : public Light {
+  public:
+    PointLight(const Point3f& pLight, const Spectrum& I) : Light(/* DeltaPosition */ 1, 1), pLight(pLight), I(I) {}
+    const Point3f& GetPosition() const { return pLight; }  // PATCH
+    const Spectrum& GetIntensity() const { return I; }     // PATCH
+  private:
+    const Point3f pLight;
+    const Spectrum I;
+};
+
+// lights/infinite.h:52-76 with a constant radiance (no "mapname"): the 1x1
+// Lmap texel L * scale (infinite.cpp:43-61)
+class InfiniteAreaLight : public Light {
+  public:
+    InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& L, int nSamples)
+        : Light(/* Infinite */ 8, nSamples), LightToWorld(LightToWorld), texel(L) {}
+    // PATCH: LightToWorld (light.h protected member) and the constant texel
+    // (nullptr return for an image map, which the binding refuses)
+    const Transform& GetLightToWorld() const { return LightToWorld; }
+    const Spectrum* ConstantRadiance() const { return &texel; }
+  private:
+    const Transform LightToWorld;
+    const Spectrum texel;
 };
 
 // lights/portal_arealight.h

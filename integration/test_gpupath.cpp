@@ -1,10 +1,12 @@
 // test_gpupath.cpp -- drives the GpuPathIntegrator binding the way pbrt-v3
 // would: the scene is turned into reference-style objects (TriangleMesh /
-// Triangle / AAPlaneShape shapes, MatteMaterial with ConstantTextures,
-// DiffuseAreaLight / PortalArealight with AAPortals, GeometricPrimitives in a
+// Triangle / AAPlaneShape / Sphere shapes, Matte / Metal / Glass / Mirror /
+// Plastic materials with ConstantTextures, DiffuseAreaLight / PortalArealight
+// with AAPortals / PointLight / InfiniteAreaLight, GeometricPrimitives in a
 // BVHAccel holding the reference-order SAH build, Scene, Film, Camera and the
-// RenderOptions ParamSets), GpuPathIntegrator::Render(scene) renders it, and
-// the image is compared with pt_render of the loader's own description.
+// RenderOptions ParamSets), the "gpupath" or "gpudirectlighting" integrator
+// (by the scene's Integrator) renders it through Render(scene), and the image
+// is compared with pt_render of the loader's own description.
 //
 //   test_gpupath scene.pbrt binding.pfm direct.pfm
 //
@@ -15,9 +17,17 @@
 
 #include "gpupath.h"
 #include "accelerators/bvh.h"
+#include "lights/infinite.h"
+#include "lights/point.h"
 #include "lights/portal_arealight.h"
+#include "materials/dispersive_glass.h"
+#include "materials/glass.h"
 #include "materials/matte.h"
+#include "materials/metal.h"
+#include "materials/mirror.h"
+#include "materials/plastic.h"
 #include "shapes/plane.h"
+#include "shapes/sphere.h"
 #include "shapes/triangle.h"
 #include "textures/constant.h"
 
@@ -97,13 +107,42 @@ int main(int argc, char** argv) {
                                                        Point3f(p.lo[0], p.lo[1], p.lo[2]),
                                                        Point3f(p.hi[0], p.hi[1], p.hi[2]), p.axis, true);
     }
+    std::vector<std::shared_ptr<Sphere>> sphereShape(d.n_spheres);
+    for (int i = 0; i < d.n_spheres; ++i) {
+        const pt_sphere& p = d.spheres[i];
+        auto o2w = std::make_shared<Transform>(xf(p.object_to_world));
+        pt_transform inv;
+        std::memcpy(inv.m, p.object_to_world.minv, 64);
+        std::memcpy(inv.minv, p.object_to_world.m, 64);
+        auto w2o = std::make_shared<Transform>(xf(inv));
+        keep.push_back(o2w);
+        keep.push_back(w2o);
+        sphereShape[i] = std::make_shared<Sphere>(o2w.get(), w2o.get(), (p.flags & PT_TRI_REVERSE_ORIENTATION) != 0,
+                                                  p.radius, p.zmin, p.zmax, p.phimax);
+    }
+    // materials: constant textures holding the loader's values; the microfacet
+    // ones carry alpha already remapped, so remapRoughness = false
+    auto cs = [](const float* v) { return std::make_shared<ConstantTexture<Spectrum>>(Spectrum::FromRGB(v)); };
+    auto cf = [](float v) { return std::make_shared<ConstantTexture<Float>>(v); };
     std::vector<std::shared_ptr<Material>> mats(d.n_materials);
     for (int i = 0; i < d.n_materials; ++i) {
         const pt_material& m = d.materials[i];
         if (m.kind == PT_MAT_MATTE)
-            mats[i] = std::make_shared<MatteMaterial>(
-                std::make_shared<ConstantTexture<Spectrum>>(Spectrum::FromRGB(m.kd)),
-                std::make_shared<ConstantTexture<Float>>(m.sigma), nullptr);
+            mats[i] = std::make_shared<MatteMaterial>(cs(m.kd), cf(m.sigma), nullptr);
+        else if (m.kind == PT_MAT_METAL)
+            mats[i] = std::make_shared<MetalMaterial>(cs(m.eta), cs(m.k), cf(m.alpha[0]), cf(m.alpha[0]), cf(m.alpha[1]),
+                                                      nullptr, false);
+        else if (m.kind == PT_MAT_GLASS)
+            mats[i] = std::make_shared<GlassMaterial>(cs(m.kr), cs(m.kt), cf(m.specular ? 0.f : m.alpha[0]),
+                                                      cf(m.specular ? 0.f : m.alpha[1]), cf(m.ior), nullptr, false);
+        else if (m.kind == PT_MAT_DISPERSIVE_GLASS)
+            mats[i] = std::make_shared<DispersiveGlassMaterial>(cs(m.kr), cs(m.kt), cf(m.specular ? 0.f : m.alpha[0]),
+                                                                cf(m.specular ? 0.f : m.alpha[1]), cf(m.ior_min),
+                                                                cf(m.ior_max), nullptr, false);
+        else if (m.kind == PT_MAT_MIRROR)
+            mats[i] = std::make_shared<MirrorMaterial>(cs(m.kr), nullptr);
+        else if (m.kind == PT_MAT_PLASTIC)
+            mats[i] = std::make_shared<PlasticMaterial>(cs(m.kd), cs(m.ks), cf(m.alpha[0]), nullptr, false);
         else if (m.kind != PT_MAT_NONE) {
             std::fprintf(stderr, "test_gpupath: material kind %d is not built by this driver\n", m.kind);
             return 1;
@@ -128,6 +167,20 @@ int main(int argc, char** argv) {
                                                               st, l.two_sided != 0);
         } else if (l.kind == PT_LIGHT_DIFFUSE_AREA) {
             areaLights[i] = std::make_shared<DiffuseAreaLight>(L, l.n_samples, triShape[l.shape], l.two_sided != 0);
+        } else if (l.kind == PT_LIGHT_DIFFUSE_SPHERE) {
+            areaLights[i] = std::make_shared<DiffuseAreaLight>(L, l.n_samples, sphereShape[l.shape], l.two_sided != 0);
+        } else if (l.kind == PT_LIGHT_DIFFUSE_PLANE) {
+            areaLights[i] = std::make_shared<DiffuseAreaLight>(L, l.n_samples, planeShape[l.shape], l.two_sided != 0);
+        } else if (l.kind == PT_LIGHT_POINT) {
+            // pLight = LightToWorld(Point3f(0, 0, 0)) (point.h:55; Transform::operator()(Point3f))
+            const float* m = l.light_to_world.m;
+            Point3f p(m[3], m[7], m[11]);
+            if (m[15] != 1) p = Point3f(m[3] / m[15], m[7] / m[15], m[11] / m[15]);
+            lights.push_back(std::make_shared<PointLight>(p, L));
+            continue;
+        } else if (l.kind == PT_LIGHT_INFINITE) {
+            lights.push_back(std::make_shared<InfiniteAreaLight>(xf(l.light_to_world), L, l.n_samples));
+            continue;
         } else {
             std::fprintf(stderr, "test_gpupath: light kind %d is not built by this driver\n", l.kind);
             return 1;
@@ -145,6 +198,10 @@ int main(int argc, char** argv) {
             const pt_aaplane& pl = d.planes[p.index];
             prims.push_back(std::make_shared<GeometricPrimitive>(
                 planeShape[p.index], mats[pl.material], pl.area_light >= 0 ? areaLights[pl.area_light] : nullptr));
+        } else if (p.kind == PT_PRIM_SPHERE) {
+            const pt_sphere& sp = d.spheres[p.index];
+            prims.push_back(std::make_shared<GeometricPrimitive>(
+                sphereShape[p.index], mats[sp.material], sp.area_light >= 0 ? areaLights[sp.area_light] : nullptr));
         } else {
             std::fprintf(stderr, "test_gpupath: prim kind %d is not built by this driver\n", p.kind);
             return 1;
@@ -177,6 +234,7 @@ int main(int argc, char** argv) {
     samplerPs.AddInt("pixelsamples", {d.sampler.spp});
     samplerPs.AddBool("samplepixelcenter", d.sampler.sample_pixel_center != 0);
     integratorPs.AddInt("maxdepth", {d.integrator.max_depth});
+    integratorPs.AddString("strategy", d.integrator.direct_strategy == PT_DIRECT_ONE ? "one" : "all");
     integratorPs.AddFloat("rrthreshold", {d.integrator.rr_threshold});
     integratorPs.AddString("lightsamplestrategy", d.integrator.light_strategy == PT_LIGHTS_POWER ? "power" : "uniform");
     if (d.integrator.has_pixel_bounds)
@@ -186,9 +244,18 @@ int main(int argc, char** argv) {
                           std::unique_ptr<Filter>(new Filter(Vector2f(d.film.filter_radius[0], d.film.filter_radius[1]))),
                           d.film.diagonal, argv[2]);
     auto camera = std::make_shared<Camera>(film);
-    std::unique_ptr<GpuPathIntegrator> integ(CreateGpuPathIntegrator(
-        integratorPs, cameraPs, filmPs, d.film.filter == PT_FILTER_GAUSSIAN ? "gaussian" : "box", filterPs, samplerPs,
-        xf(d.camera.camera_to_world), camera));
+    // RenderOptions::MakeIntegrator: "gpudirectlighting" for a DirectLighting scene, else "gpupath"
+    const std::string filterName = d.film.filter == PT_FILTER_GAUSSIAN ? "gaussian" : "box";
+    std::unique_ptr<GpuPathIntegrator> integ(
+        d.integrator.kind == PT_INTEGRATOR_DIRECT
+            ? CreateGpuDirectLightingIntegrator(integratorPs, cameraPs, filmPs, filterName, filterPs, samplerPs,
+                                                xf(d.camera.camera_to_world), camera)
+            : CreateGpuPathIntegrator(integratorPs, cameraPs, filmPs, filterName, filterPs, samplerPs,
+                                      xf(d.camera.camera_to_world), camera));
+    if (d.integrator.kind != PT_INTEGRATOR_PATH && d.integrator.kind != PT_INTEGRATOR_DIRECT) {
+        std::fprintf(stderr, "test_gpupath: integrator kind %d is not bound\n", d.integrator.kind);
+        return 1;
+    }
     integ->Render(scene);
     if (integ->Image().empty()) return 1;
 

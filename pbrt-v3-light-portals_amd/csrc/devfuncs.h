@@ -78,34 +78,70 @@ __device__ __forceinline__ float halton_dim(const DevScene& sc, uint32_t idx, in
 // The Halton tables of the leading DevScene::hal_lds_dims dimensions staged in
 // LDS by the shading kernel (the digit loop's permutation gathers are its
 // longest chain of dependent loads): per dimension {magic, base | first
-// permutation entry << 16, shift, 1/base} and c0, then those dimensions'
-// permutation entries.
+// permutation entry << 16, shift | shift(base^2) << 8, magic(base^2)} and
+// {c0, 1/base}, then those dimensions' permutation entries.
 struct HalLds {
     const uint4* rec;
-    const float* c0;
+    const float2* cb;
     const uint16_t* perm;
     int dims;
 };
 __device__ __forceinline__ HalLds stage_halton(const DevScene& sc, uint4* lds) {
     const int D = sc.hal_lds_dims;
     uint4* rec = lds;
-    float* c0 = (float*)(lds + D);
-    uint16_t* perm = (uint16_t*)(c0 + D);
+    float2* cb = (float2*)(lds + D);
+    uint16_t* perm = (uint16_t*)(cb + D);
     for (int i = threadIdx.x; i < D; i += blockDim.x) {
         const DivMagic dm = sc.divs[i];
-        rec[i] = make_uint4(dm.magic, dm.base | ((uint32_t)sc.prime_sums[i] << 16), dm.shift, __float_as_uint(dm.inv_base));
-        c0[i] = sc.perm_c0[i];
+        const DivMagic d2 = sc.divs2[i];
+        rec[i] = make_uint4(dm.magic, dm.base | ((uint32_t)sc.prime_sums[i] << 16), dm.shift | (d2.shift << 8), d2.magic);
+        cb[i] = make_float2(sc.perm_c0[i], dm.inv_base);
     }
     for (int i = threadIdx.x; i < sc.hal_lds_perm; i += blockDim.x) perm[i] = sc.perm[i];
     __syncthreads();
-    return HalLds{rec, c0, perm, D};
+    return HalLds{rec, cb, perm, D};
+}
+// ScrambledRadicalInverseSpecialized (lowdiscrepancy.cpp:405-424) two digits
+// per step: one division by base^2 gives both (q = d0 + base * d1), and
+// (rev * base + perm[d0]) * base + perm[d1] == rev * base^2 + (perm[d0] * base
+// + perm[d1]) exactly in the integer accumulator; invBaseN keeps the
+// reference's one float multiply per digit.  The loop runs exactly the
+// number of digit pairs (no masked slots); an odd last digit is a itself.
+template <typename Rev>
+__device__ __forceinline__ float scrambled_ri_pairs(float c0, float invBase, uint32_t a, const DivMagic& dm,
+                                                    const DivMagic& d2, const uint16_t* perm) {
+    Rev rev = 0;
+    float invBaseN = 1;
+    while (a >= dm.base) {
+        const uint32_t next = fast_div(a, d2);
+        const uint32_t q = a - next * d2.base;
+        const uint32_t d1 = fast_div(q, dm);
+        const uint32_t d0 = q - d1 * dm.base;
+        const uint32_t p0 = perm[d0], p1 = perm[d1];
+        rev = rev * (Rev)d2.base + ((Rev)p0 * (Rev)dm.base + (Rev)p1);
+        invBaseN *= invBase;
+        invBaseN *= invBase;
+        a = next;
+    }
+    if (a) {
+        rev = rev * (Rev)dm.base + (Rev)perm[a];
+        invBaseN *= invBase;
+    }
+    return smin(invBaseN * ((float)rev + c0), kOneMinusEps);
 }
 // halton_dim with the staged tables for dimensions below hl.dims.
 __device__ __forceinline__ float halton_dim(const DevScene& sc, const HalLds& hl, uint32_t idx, int dim) {
     if (dim < 2 || dim >= hl.dims) return halton_dim(sc, idx, dim);
     const uint4 r = hl.rec[dim];
-    const DivMagic dm{r.y & 0xffffu, r.x, r.z, __uint_as_float(r.w)};
-    return scrambled_radical_inverse(dm, hl.perm + (r.y >> 16), hl.c0[dim], idx);
+    const float2 cb = hl.cb[dim];
+    const uint32_t b = r.y & 0xffffu;
+    const DivMagic dm{b, r.x, r.z & 0xffu, cb.y};
+    const DivMagic d2{b * b, r.w, r.z >> 8, 0.f};
+    const uint16_t* perm = hl.perm + (r.y >> 16);
+    // rev < base^nDigits <= base * a: below 2^32 the reference's 64-bit
+    // accumulator never leaves 32 bits
+    if ((uint64_t)idx * b < (1ull << 32)) return scrambled_ri_pairs<uint32_t>(cb.x, cb.y, idx, dm, d2, perm);
+    return scrambled_ri_pairs<uint64_t>(cb.x, cb.y, idx, dm, d2, perm);
 }
 
 // Per-pixel Halton offset (halton.cpp:96-113); values stay far below 2^32.

@@ -118,6 +118,7 @@ struct DevScene {
     const uint16_t* perm;
     const int* prime_sums;
     const DivMagic* divs;   // per dimension: prime base, magic, shift, 1/base
+    const DivMagic* divs2;  // per dimension: division by base^2 (two digits per step, staged tables)
     const float* perm_c0;   // per dimension: invBase * perm[0] / (1 - invBase)
     int max_dim;
     int hal_lds_dims;       // leading dimensions whose tables the shading kernel stages in LDS (0: none)

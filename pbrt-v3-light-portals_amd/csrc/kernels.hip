@@ -773,7 +773,8 @@ __device__ __forceinline__ S3 hit_Le(const DevScene& sc, int prim, const Ray& ra
 // loads them one path ahead.
 struct NeeIn {
     S3 F, Li, beta;
-    float pdf, lpdf;
+    float pdf, lpdf;  // pdf: the portal estimators' sample pdf; MIS ray B: the scattering pdf
+    float w;          // projection: the portal-selection pdf; MIS ray B: the scattering weight
     int nl;   // MIS: the light the BSDF-sampled ray B must hit
     Ray ray;
 };
@@ -782,7 +783,7 @@ struct NeeIn {
 __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uint32_t fl, int hA) {
     const uint32_t N = (uint32_t)ps.n;
     const float* nee = ps.nee;
-    NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, 0, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
+    NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, 1.f, 0, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
     const bool portalA = (fl & kNfPortal) && (fl & kNfA);
     const bool misB = !(fl & kNfPortal) && (fl & kNfMis) && (fl & kNfB);
     const bool mis = !(fl & kNfPortal) && (fl & kNfMis);
@@ -793,9 +794,12 @@ __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uin
     if ((portalA && hA < 0) || misB)
         in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
     if (portalA) in.pdf = nee[kNeePdf * N + slot];
+    if ((fl & kNfPortal) && (fl & kNfDivPortal)) in.w = nee[kNeePortalPdf * N + slot];
     if (portalA && hA >= 0) in.ray = load_ray6(ps.rayA, N, slot, kInf);
     if (misB) {
         in.nl = __float_as_int(nee[kNeeLight * N + slot]);
+        in.w = nee[kNeeSw * N + slot];
+        in.pdf = nee[kNeeSpdf * N + slot];
         in.ray = load_ray6(ps.rayB, N, slot, kInf);
     }
     return in;
@@ -818,7 +822,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
             const S3 f = in.F;
             if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / in.pdf;
         }
-        if (fl & kNfDivPortal) Ld = Ld / nee[kNeePortalPdf * N + slot];
+        if (fl & kNfDivPortal) Ld = Ld / in.w;
     } else if (fl & kNfMis) {
         if ((fl & kNfC1) && hA == 0) Ld = Ld + in.F;
         if (fl & kNfB) {
@@ -834,7 +838,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
             }
             if (!is_black(Li)) {
                 const S3 f2 = in.Li;
-                Ld = Ld + (((f2 * Li) * s3(1.f)) * nee[kNeeSw * N + slot]) / nee[kNeeSpdf * N + slot];
+                Ld = Ld + (((f2 * Li) * s3(1.f)) * in.w) / in.pdf;
             }
         }
     }
@@ -1044,6 +1048,7 @@ struct PathPre {
     S3 L, beta;
     Ray ray;
     NeeIn nee;
+    float eta;    // etaScale (Russian roulette reads it)
     PrimRec rec;  // the hit primitive's record (loaded once `hit` is in)
 };
 // Two stages: the head (state word, payload flags, hits) two paths ahead, the
@@ -1062,6 +1067,7 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
         p->hidx = ps.hidx[slot];
         p->beta = load_s3(ps.beta, N, slot);
         p->ray = load_ray6(ps.ray, N, slot, kInf);
+        p->eta = ps.eta[slot];
     }
     if (p->st & kStNee) p->nee = nee_load(ps, slot, p->nfl, p->hitA);
 }
@@ -1178,16 +1184,18 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     beta = beta * ((f * absdot(wi, si.sn)) / pdf);
                     if (sampled & kBxSpecular) st |= kStSpecular;
                     else st &= ~kStSpecular;
+                    float etaScale = pre.eta;
                     if (Ft<kFt>::spec && (sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
                         const float eta = bsdf.eta;
-                        ps.eta[slot] *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                        etaScale *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
+                        ps.eta[slot] = etaScale;
                         *ab += 4;
                     }
                     *ab += 4;  // etaScale read for Russian roulette
                     const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     bool alive = true;
                     // Russian roulette (path.cpp:177-185)
-                    const S3 rrBeta = beta * ps.eta[slot];
+                    const S3 rrBeta = beta * etaScale;
                     if (max_comp(rrBeta) < sc.rr_threshold && bounces > 3) {
                         const float q = smax(0.05f, 1 - max_comp(rrBeta));
                         if (dm.get1() < q) alive = false;
@@ -1738,9 +1746,15 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
 __global__ void k_debug_halton(DevScene sc, const uint32_t* idx, const int* dims, int n, float* out)
 #ifdef PT_TU_MISC
 {
+    // both table paths: the shading kernel's LDS-staged one (two digits per
+    // step) is returned; a disagreement with the global-table path is a NaN
+    extern __shared__ uint4 dbg_lds[];
+    const HalLds hl = stage_halton(sc, dbg_lds);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = dims[i] < sc.max_dim ? halton_dim(sc, idx[i], dims[i]) : -1.f;
+    if (dims[i] >= sc.max_dim) { out[i] = -1.f; return; }
+    const float a = halton_dim(sc, hl, idx[i], dims[i]), b = halton_dim(sc, idx[i], dims[i]);
+    out[i] = __float_as_uint(a) == __float_as_uint(b) ? a : __uint_as_float(0x7fc00000u);
 }
 #else
 ;

@@ -240,7 +240,7 @@ struct pt_scene {
     pt::DBuf<pt::DevLight> lights;
     pt::DBuf<uint16_t> perm;
     pt::DBuf<int> psums;
-    pt::DBuf<pt::DivMagic> divs;
+    pt::DBuf<pt::DivMagic> divs, divs2;
     pt::DevScene dev{};
     // hero integrators (SampledSpectrum scenes): tables, light distributions, per-slot radiance
     bool hero = false;
@@ -912,10 +912,11 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     // recursion's dimensions depend on the scene, so keep every prime.
     const bool direct = d->integrator.kind == PT_INTEGRATOR_DIRECT;
     int max_dim = direct ? 1000 : std::min(1000, 6 + 8 * (d->integrator.max_depth + 1));
-    std::vector<DivMagic> divs((size_t)max_dim);
+    std::vector<DivMagic> divs((size_t)max_dim), divs2((size_t)max_dim);
     std::vector<float> c0((size_t)max_dim);
     for (int i = 0; i < max_dim; ++i) {
         divs[i] = make_div_magic((uint32_t)ht.primes[i]);
+        divs2[i] = make_div_magic((uint32_t)ht.primes[i] * (uint32_t)ht.primes[i]);
         const float invBase = (float)1 / (float)ht.primes[i];
         c0[i] = invBase * (float)ht.perms[(size_t)ht.prime_sums[i]] / (1 - invBase);
     }
@@ -923,6 +924,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     s->perm.upload(ht.perms.data(), nperm);
     s->psums.upload(ht.prime_sums.data(), (size_t)max_dim);
     s->divs.upload(divs);
+    s->divs2.upload(divs2);
     s->perm_c0.upload(c0);
     s->spp = d->sampler.spp;
 
@@ -963,6 +965,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     ds.perm = s->perm.p;
     ds.prime_sums = s->psums.p;
     ds.divs = s->divs.p;
+    ds.divs2 = s->divs2.p;
     ds.perm_c0 = s->perm_c0.p;
     ds.max_dim = max_dim;
     // the shading kernel stages the leading dimensions' tables in LDS: as many as fit kHalLdsMax
@@ -972,11 +975,11 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
         const char* e = std::getenv("PT_HAL_LDS");
         if (!(e && e[0] == '0'))
             while (D < max_dim && D < (int)ht.prime_sums.size() - 1 &&
-                   (size_t)20 * (D + 1) + 2 * (size_t)ht.prime_sums[D + 1] <= kHalLdsMax && ht.prime_sums[D + 1] < 65536)
+                   (size_t)24 * (D + 1) + 2 * (size_t)ht.prime_sums[D + 1] <= kHalLdsMax && ht.prime_sums[D + 1] < 65536)
                 ++D;
         ds.hal_lds_dims = D;
         ds.hal_lds_perm = D > 0 ? ht.prime_sums[D] : 0;
-        ds.hal_lds_bytes = (int)tab_align16(D > 0 ? (uint32_t)(20 * D + 2 * ds.hal_lds_perm) : 0u);
+        ds.hal_lds_bytes = (int)tab_align16(D > 0 ? (uint32_t)(24 * D + 2 * ds.hal_lds_perm) : 0u);
         s->hal_lds_bytes = (size_t)ds.hal_lds_bytes;
         // k_shade_tab: the scene tables after them, when they fit kTabLdsMax (PT_SHADE_TAB=0 disables)
         const TabLayout tl = tab_layout((int)s->host_prim_order.size(), d->n_materials, nl, d->n_planes, d->n_portals);
@@ -1948,7 +1951,8 @@ pt_status pt_debug_halton(pt_scene* s, int n, const uint32_t* idx, const int32_t
     return guarded([&] {
         DBuf<uint32_t> di; DBuf<int> dd; DBuf<float> o;
         di.upload(idx, (size_t)n); dd.upload(dims, (size_t)n); o.alloc((size_t)n);
-        hipLaunchKernelGGL(k_debug_halton, dim3(ceil_div(n, 256)), dim3(256), 0, 0, s->dev, di.p, dd.p, n, o.p);
+        hipLaunchKernelGGL(k_debug_halton, dim3(ceil_div(n, 256)), dim3(256), (size_t)s->dev.hal_lds_bytes, 0, s->dev,
+                           di.p, dd.p, n, o.p);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpy(out, o.p, sizeof(float) * n, hipMemcpyDeviceToHost));
     });

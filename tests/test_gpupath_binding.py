@@ -1,8 +1,10 @@
 """The reference-side drop-in (integration/gpupath.{h,cpp}): a pbrt-v3
 Integrator whose Render(const Scene&) flattens the reference's own scene
-objects -- BVHAccel of GeometricPrimitives (Triangle / AAPlaneShape),
-MatteMaterial, DiffuseAreaLight / PortalArealight + AAPortals -- into
-pt_scene_desc (prebuilt BVH included) and renders through the C ABI.
+objects -- BVHAccel of GeometricPrimitives (Triangle / AAPlaneShape /
+Sphere), Matte / Metal / Glass / Mirror / Plastic materials, DiffuseAreaLight
+(triangle, sphere, aaplane) / PortalArealight + AAPortals / PointLight /
+constant InfiniteAreaLight -- into pt_scene_desc (prebuilt BVH included) and
+renders through the C ABI, as "gpupath" or "gpudirectlighting".
 
 CPU: the binding compiles against stub pbrt headers that mirror the
 reference's classes (integration/pbrt_stub) and the C header.  GPU: the
@@ -56,3 +58,33 @@ def test_render_through_binding_matches_c_abi(tmp_path, kind):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("identical")
     assert os.path.getsize(tmp_path / "binding.pfm") == os.path.getsize(tmp_path / "direct.pfm")
+
+
+# The reference's own scenes through Render(const Scene&) (reference scene
+# files imported verbatim): lamp (DirectLighting, MetalMaterial, plymesh with
+# normals and uv, two portals), sandbox (DirectLighting, PointLight, a
+# PortalArealight under a rotated Transform), creeper (PointLight, a
+# DiffuseAreaLight on an aaplane, Scale -1 1 1 before LookAt),
+# cornell_dielectric as path (glass, a constant infinite light) and
+# killeroo-simple as path (plastic, a sphere area light).
+REFERENCE_SCENES = {
+    "lamp": dict(name="lamp/lamp.pbrt", res=(64, 64), spp=2),
+    "lamp-path": dict(name="lamp/lamp.pbrt", res=(64, 64), spp=2,
+                      extra=[('Integrator "directlighting"', 'Integrator "path" "integer maxdepth" [5]'),
+                             ('"integer maxdepth" [100]', '')]),
+    "sandbox": dict(name="creeper/sandbox.pbrt", res=(96, 96), spp=2),
+    "creeper": dict(name="creeper/creeper.pbrt", res=(96, 96), spp=2),
+    "cornell-dielectric-path": dict(name="cornell_dielectric.pbrt", res=(48, 48), spp=4),
+    "killeroo-path": dict(name="killeroo-simple.pbrt", res=(48, 48), spp=2,
+                          extra=[('Integrator "mypath"', 'Integrator "path"')]),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", sorted(REFERENCE_SCENES))
+def test_reference_scenes_through_binding(tmp_path, which):
+    scene = scene_variant(tmp_path, **REFERENCE_SCENES[which])
+    r = subprocess.run([DRIVER, scene, str(tmp_path / "binding.pfm"), str(tmp_path / "direct.pfm")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("identical"), r.stdout
