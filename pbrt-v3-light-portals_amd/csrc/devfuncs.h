@@ -726,7 +726,10 @@ enum : int {
     kFtSpecular = 2,    // smooth glass, dispersive glass, mirror: specular lobes
     kFtInfinite = 4,    // an InfiniteAreaLight
     kFtSphere = 8,      // Sphere shapes (and sphere area lights)
-    kFtAll = 15
+    kFtAll = 15,
+    // a reduction, outside kFtAll: every light is a PortalArealight, so the
+    // path kernel leaves EstimateDirect's MIS branch out (fewer live registers)
+    kFtPortalOnly = 16
 };
 template <int kFt>
 struct Ft {
@@ -734,6 +737,7 @@ struct Ft {
     static constexpr bool spec = (kFt & kFtSpecular) != 0;
     static constexpr bool inf = (kFt & kFtInfinite) != 0;
     static constexpr bool sph = (kFt & kFtSphere) != 0;
+    static constexpr bool mis = (kFt & kFtPortalOnly) == 0;  // lights sampled by the MIS branch may occur
     static constexpr int max_lobes = (micro || spec) ? 2 : 1;
 };
 

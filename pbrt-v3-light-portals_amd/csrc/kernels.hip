@@ -823,7 +823,7 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
             if (!is_black(f) && !is_black(Li)) Ld = Ld + (f * Li) / in.pdf;
         }
         if (fl & kNfDivPortal) Ld = Ld / in.w;
-    } else if (fl & kNfMis) {
+    } else if (Ft<kFt>::mis && (fl & kNfMis)) {
         if ((fl & kNfC1) && hA == 0) Ld = Ld + in.F;
         if (fl & kNfB) {
             const int h = hB;
@@ -1047,10 +1047,23 @@ struct PathPre {
     uint32_t nfl;
     S3 L, beta;
     Ray ray;
-    NeeIn nee;
     float eta;    // etaScale (Russian roulette reads it)
-    PrimRec rec;  // the hit primitive's record (loaded once `hit` is in)
 };
+// What a step reads of its own path only once it starts: the NEE payload
+// and the hit primitive's record.  shade_batch issues these loads before the
+// next path's body prefetch, so waiting for them (vmcnt counts in issue
+// order) does not wait for the prefetch, and they are not carried in
+// registers through the previous step (the register budget of 3 waves).
+struct PathNow {
+    NeeIn nee;
+    PrimRec rec;
+};
+template <bool kTab>
+__device__ __forceinline__ void path_load_now(const DevScene& sc, const DevPaths& ps, uint32_t slot, const PathPre& p,
+                                              PathNow* q) {
+    if (p.st & kStNee) q->nee = nee_load(ps, slot, p.nfl, p.hitA);
+    if ((p.st & kStCont) && p.hit >= 0) q->rec = prim_rec(sc, p.hit);
+}
 // Two stages: the head (state word, payload flags, hits) two paths ahead, the
 // body one path ahead and only what the head says this step will read.
 __device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t slot, PathPre* p) {
@@ -1069,10 +1082,6 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
         p->ray = load_ray6(ps.ray, N, slot, kInf);
         p->eta = ps.eta[slot];
     }
-    if (p->st & kStNee) p->nee = nee_load(ps, slot, p->nfl, p->hitA);
-}
-__device__ __forceinline__ void path_prefetch_prim(const DevScene& sc, PathPre* p) {
-    if ((p->st & kStCont) && p->hit >= 0) p->rec = prim_rec(sc, p->hit);
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
@@ -1080,8 +1089,8 @@ __device__ __forceinline__ void path_prefetch_prim(const DevScene& sc, PathPre* 
 // vertex to the next, plus the queue entries (scene tables are not counted).
 template <int kFt>
 __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl, const DevPaths& ps, uint32_t slot,
-                                           const PathPre& pre, uint32_t* rays, uint32_t* nrays, bool* keep,
-                                           bool* overflow, uint32_t* ab) {
+                                           const PathPre& pre, const PathNow& now, uint32_t* rays, uint32_t* nrays,
+                                           bool* keep, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     *nrays = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
@@ -1101,7 +1110,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
             }
             *ab += b;
         }
-        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.hitB, pre.nee, &L);
+        resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.hitB, now.nee, &L);
         st &= ~kStNee;
     }
     if (st & kStCont) {
@@ -1113,9 +1122,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
         S3 beta = pre.beta;
         *ab += 24 + 4 + 12;
         SurfHit si;
-        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, pre.rec, ray, &si);
+        bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, now.rec, ray, &si);
         int mat = -1, light = -1;
-        if (found) prim_info<Ft<kFt>::sph>(sc, pre.rec, &mat, &light);
+        if (found) prim_info<Ft<kFt>::sph>(sc, now.rec, &mat, &light);
         if (bounces == 0 || specular) {
             if (found) L = L + beta * (light >= 0 ? area_L(sc.lights[PT_IDX(light, sc.n_lights)], si.n, -ray.d) : s3(0.f));
             else if (Ft<kFt>::inf)
@@ -1151,7 +1160,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                             haveLight = true;
                             const float uL0 = dm.get1(), uL1 = dm.get1();
                             const float uS0 = dm.get1(), uS1 = dm.get1();
-                            if (sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
+                            if (!Ft<kFt>::mis || sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
                                 if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1, ab)) {
                                     rays[(*nrays)++] = slot << 2 | kRayA;
                                     deferred = true;
@@ -1273,6 +1282,26 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
     // ahead and the body of the next path are in flight (slots in the queue
     // are distinct, so no step writes what a prefetch read)
     uint32_t base = blockIdx.x * blockDim.x;
+#if defined(PT_SHADE_PIPE) && PT_SHADE_PIPE == 0
+    // experiment build: no prefetch (each path's loads, then its step)
+    for (; base < n; base += stride) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t rays[3];
+        uint32_t nrays = 0;
+        bool keep = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = pq[i];
+            PathPre pre{};
+            PathNow now{};
+            path_prefetch_head(ps, slot, &pre);
+            path_prefetch_body(ps, slot, &pre);
+            path_load_now<kTab>(sc, ps, slot, pre, &now);
+            shade_path<kFt>(sc, hl, ps, slot, pre, now, rays, &nrays, &keep, &overflow, &ab);
+        }
+        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+    }
+#else
     const uint32_t i0 = base + threadIdx.x;
     uint32_t slot = 0, slot1 = 0, slot2 = 0;
     PathPre pre{}, nxt{};  // this path (complete) and the next one (head only)
@@ -1280,7 +1309,6 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         slot = pq[i0];
         path_prefetch_head(ps, slot, &pre);
         path_prefetch_body(ps, slot, &pre);
-        path_prefetch_prim(sc, &pre);
     }
     if (i0 + stride < n) {
         slot1 = pq[i0 + stride];
@@ -1290,15 +1318,16 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
     for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
         PathPre nn{};
+        PathNow now{};
         uint32_t slot3 = 0;
+        if (i < n) path_load_now<kTab>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
         if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
         if (i + 2 * stride < n) path_prefetch_head(ps, slot2, &nn);
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
         uint32_t rays[3];
         uint32_t nrays = 0;
         bool keep = false;
-        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, rays, &nrays, &keep, &overflow, &ab);
-        if (i + stride < n) path_prefetch_prim(sc, &nxt);  // nxt.hit has arrived by now
+        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, rays, &nrays, &keep, &overflow, &ab);
         wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;
         slot1 = slot2;
@@ -1306,6 +1335,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         pre = nxt;
         nxt = nn;
     }
+#endif
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
     const unsigned long long abw = wave_sum_u64((unsigned long long)ab);
@@ -1623,13 +1653,14 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_tab(DevScene sc, DevPaths
 #else
 ;
 #endif
+// k_shade_tab with a 3-waves-per-SIMD register budget (PT_SHADE_VARIANT=3)
 template <int kFt>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, false>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, true>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;

@@ -264,7 +264,7 @@ struct pt_scene {
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
     bool shade_tab = false;      // k_shade_tab: the scene tables staged in LDS as well (small scenes)
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
-    int shade_variant = 0;       // 0: compiler register budget (no scratch), 3/4: forced waves per SIMD
+    int shade_variant = 0;       // 0: compiler register budget (no scratch), 3: k_shade_tab at 3 waves per SIMD
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
@@ -312,6 +312,9 @@ static int scene_features(const pt_scene_desc* d) {
     for (int i = 0; i < d->n_lights; ++i)
         if (d->lights[i].kind == PT_LIGHT_INFINITE) f |= kFtInfinite;
     if (d->n_spheres > 0) f |= kFtSphere;
+    bool portalOnly = d->n_lights > 0;
+    for (int i = 0; i < d->n_lights; ++i) portalOnly &= d->lights[i].kind == PT_LIGHT_PORTAL_AREA;
+    if (portalOnly) f |= kFtPortalOnly;
     return f;
 }
 
@@ -328,6 +331,7 @@ static ShadeKernel shade_kernel_ft(int variant) {
 // Instantiated feature sets: all-matte, + infinite light, + spheres, + both,
 // everything.  Other combinations take the full kernel.
 static ShadeKernel shade_kernel(int variant, int features) {
+    if (features == kFtPortalOnly) return shade_kernel_ft<kFtPortalOnly>(variant);  // matte, portal lights only
     switch (features & kFtAll) {
         case 0: return shade_kernel_ft<0>(variant);
         case kFtInfinite: return shade_kernel_ft<kFtInfinite>(variant);

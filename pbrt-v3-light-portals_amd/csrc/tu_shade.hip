@@ -1,6 +1,7 @@
 // tu_shade.hip -- translation unit of the path-vertex shading kernels
 // (kernels.hip), one object per scene-feature set: compiled with
-// -DPT_FT=<kFt> (all instantiated feature sets when PT_FT is undefined).
+// -DPT_FT=<kFt> (all instantiated feature sets when PT_FT is undefined;
+// 99: the DirectLighting kernel).
 #define PT_TU_SHADE 1
 #include "kernels.hip"
 
@@ -26,6 +27,9 @@ PT_SHADE_FT(kFtInfinite | kFtSphere)
 PT_SHADE_FT(kFtAll)
 #endif
 #if !defined(PT_FT) || PT_FT == 16
+PT_SHADE_FT(kFtPortalOnly)
+#endif
+#if !defined(PT_FT) || PT_FT == 99
 template __global__ void k_shade_dl<kFtAll>(PT_ARGS);
 #endif
 #undef PT_SHADE_FT
