@@ -21,6 +21,7 @@ constexpr int kNodeSteps = PT_NODE_STEPS;
 constexpr int kLeafSteps = PT_LEAF_STEPS;
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kShadeBlock = 128;
+constexpr int kShadeBpcW3 = 24;       // k_shade_w3 blocks per CU (four rounds of its 6 resident blocks)
 constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h
 constexpr int kLdsSceneMax = 16384;  // bytes of BVH nodes + prim records staged in LDS by k_trace<true>
 constexpr size_t kTabLdsMax = 8192;   // bytes of scene tables k_shade_tab stages in LDS after the Halton tables

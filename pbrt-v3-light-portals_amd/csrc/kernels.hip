@@ -614,23 +614,24 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
 #pragma unroll
             for (int u = 0; u < kNodeSteps; ++u) {
                 if (u > 0 && (done || leafPos < leafEnd)) continue;
+                const bool go = true;
                 const int c = cur;
                 const float4 a = bnodes[2 * c];
                 const float4 b = bnodes[2 * c + 1];
-                ++nodes;
+                nodes += go ? 1u : 0u;
                 const bool hit = node_box_hit(a, b, ray, inv, n0, n1, n2);
                 const int off = __float_as_int(b.z);
                 const uint32_t npax = __float_as_uint(b.w);
                 const int np = (int)(npax & 0xffffu);
                 const int axis = (int)(npax >> 16);
                 const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
-                const bool inner = hit && np == 0;
-                const bool leaf = hit && np > 0;
-                const bool miss = !hit;
+                const bool inner = go && hit && np == 0;
+                const bool leaf = go && hit && np > 0;
+                const bool miss = go && !hit;
                 stk[toVisit * kTraceBlock] = neg ? c + 1 : off;  // push slot (kept only for an inner node)
                 const int popv = stk[max(toVisit - 1, 0) * kTraceBlock];
                 const bool pop = miss && toVisit > 0;
-                done = miss && toVisit == 0;
+                done = go ? (miss && toVisit == 0) : done;
                 cur = inner ? (neg ? off : c + 1) : (pop ? popv : c);
                 toVisit += inner ? 1 : (pop ? -1 : 0);
                 leafPos = leaf ? off : leafPos;

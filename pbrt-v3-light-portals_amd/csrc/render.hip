@@ -264,7 +264,8 @@ struct pt_scene {
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
     bool shade_tab = false;      // k_shade_tab: the scene tables staged in LDS as well (small scenes)
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
-    int shade_variant = 0;       // 0: compiler register budget (no scratch), 3: k_shade_tab at 3 waves per SIMD
+    int shade_variant = 0;       // 0: compiler register budget, 3: k_shade_tab at 3 waves per SIMD (default when
+                                 // that build has no scratch), 5: k_shade_tab
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
@@ -1510,6 +1511,15 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) s->shade_variant = std::atoi(v);
+    else if (s->shade_tab && !s->hero) {
+        // the 3-waves-per-SIMD build of k_shade_tab when it needs no scratch (spills cost more than the
+        // third wave gains), with the grid-stride loop sized for it (PT_SHADE_BPC overrides)
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, (const void*)shade_kernel(3, s->features)) == hipSuccess && fa.localSizeBytes == 0) {
+            s->shade_variant = 3;
+            s->shade_bpc = kShadeBpcW3;
+        }
+    }
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
