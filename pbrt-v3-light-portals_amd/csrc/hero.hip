@@ -451,7 +451,7 @@ __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPa
 // shadow ray of SampleEmitterHero and the next continuation ray.
 template <int kFt>
 __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, const DevPaths& ps, const DevHeroPaths& hp,
-                          uint32_t slot, uint32_t* rays, uint32_t* nrays, bool* overflow, uint32_t* ab) {
+                          uint32_t slot, RayList* rays, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
     uint32_t st = ps.st[slot];
     float* Lg = hp.L + hbin_at(N, slot, 0);
@@ -460,7 +460,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     float* H = hp.hs + hs_at(N, slot, 0);
     const uint32_t BS = kAos ? 1u : N;  // bin / scalar stride
     uint32_t hf = __float_as_uint(H[kHsFlags * BS]);
-    *nrays = 0;
+    rays->n = 0;
     // algorithmic path-state bytes: each 60-bin array (L, nee, beta) counted
     // once per direction it is touched in this step (tch bits), plus the
     // scalar fields and queue entries
@@ -598,7 +598,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         } else if (M.kind == PT_MAT_NONE) {  // bounces-- ; continue
             store_ray6(ps.ray, N, slot, Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf});
             sb += 24;
-            rays[(*nrays)++] = slot << 2 | kRayCont;
+            rays->push(slot << 2 | kRayCont);
             cont = true;
         } else {
             const bool disp = M.kind == PT_MAT_DISPERSIVE_GLASS;
@@ -649,7 +649,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         a[3 * N + slot] = dd.x; a[4 * N + slot] = dd.y; a[5 * N + slot] = dd.z;
                         a[6 * N + slot] = 1 - kShadowEps;
                         sb += 28;
-                        rays[(*nrays)++] = slot << 2 | kRayShadow;
+                        rays->push(slot << 2 | kRayShadow);
                         st |= kStNee;
                         // the term as if unoccluded
                         emPdf = emPdf * epdf;
@@ -828,7 +828,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                              ((flags & kBxSpecular) ? kHfLastSpec : 0u);
                         store_ray6(ps.ray, N, slot, ray);
                         sb += 24 + 40;  // ray; H pdfs / etaScale / bsdfPdf
-                        rays[(*nrays)++] = slot << 2 | kRayCont;
+                        rays->push(slot << 2 | kRayCont);
                         cont = true;
                         ++bounces;
                         for (int k = 0; k < 4; ++k) {
@@ -849,7 +849,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     H[kHsFlags * BS] = __uint_as_float(hf);
     ps.st[slot] = st;
     if (!(st & (kStCont | kStNee))) finish();
-    sb += 4 * (*nrays + ((st & (kStCont | kStNee)) ? 1u : 0u));  // ray / path queue entries written
+    sb += 4 * (rays->n + ((st & (kStCont | kStNee)) ? 1u : 0u));  // ray / path queue entries written
     count();
 }
 
@@ -865,16 +865,15 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
     uint32_t ab = 0;  // this lane's algorithmic path-state bytes
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t rays[3];
-        uint32_t nrays = 0;
+        RayList rays;
         bool keep = false;
         uint32_t slot = 0;
         if (i < n) {
             slot = pq[i];
-            hero_step<kFt>(sc, h, ps, hp, slot, rays, &nrays, &overflow, &ab);
+            hero_step<kFt>(sc, h, ps, hp, slot, &rays, &overflow, &ab);
             keep = (ps.st[slot] & (kStCont | kStNee)) != 0;
         }
-        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+        wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);

@@ -74,10 +74,23 @@ __device__ __forceinline__ void wq_flush(WaveQ& q, uint32_t* counts2, uint32_t* 
     q.nr = 0;
     q.np = 0;
 }
+// A step's 0..3 ray-queue entries in three registers (pushed by selects: a
+// dynamically indexed array would live in scratch).
+struct RayList {
+    uint32_t r0 = 0, r1 = 0, r2 = 0;
+    uint32_t n = 0;
+    __device__ __forceinline__ void push(uint32_t e) {
+        r0 = n == 0 ? e : r0;
+        r1 = n == 1 ? e : r1;
+        r2 = n == 2 ? e : r2;
+        ++n;
+    }
+};
 // Append nrays (0..3) ray entries and, if keep, the path slot.  Reached by
 // every lane of the wave together.
-__device__ __forceinline__ void wq_push(WaveQ& q, const uint32_t* rays, uint32_t nrays, bool keep, uint32_t slot,
-                                        uint32_t* counts2, uint32_t* rq_out, uint32_t* pq_out) {
+__device__ __forceinline__ void wq_push(WaveQ& q, const RayList& rl, bool keep, uint32_t slot, uint32_t* counts2,
+                                        uint32_t* rq_out, uint32_t* pq_out) {
+    const uint32_t nrays = rl.n;
     const uint64_t b0 = __ballot((nrays & 1u) != 0);
     const uint64_t b1 = __ballot((nrays & 2u) != 0);
     const uint64_t bp = __ballot(keep);
@@ -87,9 +100,9 @@ __device__ __forceinline__ void wq_push(WaveQ& q, const uint32_t* rays, uint32_t
     const uint32_t ptot = (uint32_t)__popcll(bp);
     if (q.nr + rtot > kWqRays || q.np + ptot > kWqPaths) wq_flush(q, counts2, rq_out, pq_out);
     const uint32_t rpre = q.nr + (uint32_t)__popcll(b0 & lower) + 2u * (uint32_t)__popcll(b1 & lower);
-#pragma unroll
-    for (uint32_t k = 0; k < 3; ++k)
-        if (k < nrays) q.r[rpre + k] = rays[k];
+    if (nrays > 0) q.r[rpre] = rl.r0;
+    if (nrays > 1) q.r[rpre + 1] = rl.r1;
+    if (nrays > 2) q.r[rpre + 2] = rl.r2;
     if (keep) q.p[q.np + (uint32_t)__popcll(bp & lower)] = slot;
     q.nr += rtot;
     q.np += ptot;
@@ -1090,10 +1103,10 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
 // vertex to the next, plus the queue entries (scene tables are not counted).
 template <int kFt>
 __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl, const DevPaths& ps, uint32_t slot,
-                                           const PathPre& pre, const PathNow& now, uint32_t* rays, uint32_t* nrays,
+                                           const PathPre& pre, const PathNow& now, RayList* rays,
                                            bool* keep, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
-    *nrays = 0;
+    rays->n = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
     uint32_t st = pre.st;
     S3 L = pre.L;
@@ -1139,7 +1152,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                 store_ray6(ps.ray, N, slot, r);
                 *ab += 24;
                 st |= kStCont;
-                rays[(*nrays)++] = slot << 2 | kRayCont;
+                rays->push(slot << 2 | kRayCont);
             } else {
                 DimsL dm{&sc, &hl, pre.hidx, (int)(st & kStDimMask), false};
                 *ab += 4;
@@ -1163,13 +1176,13 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                             const float uS0 = dm.get1(), uS1 = dm.get1();
                             if (!Ft<kFt>::mis || sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
                                 if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1, ab)) {
-                                    rays[(*nrays)++] = slot << 2 | kRayA;
+                                    rays->push(slot << 2 | kRayA);
                                     deferred = true;
                                 }
                             } else {
                                 const uint32_t f = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1, ab);
-                                if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
-                                if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
+                                if (f & kNfA) rays->push(slot << 2 | kRayShadow);
+                                if (f & kNfB) rays->push(slot << 2 | kRayB);
                                 deferred = (f & (kNfA | kNfB)) != 0;
                             }
                         }
@@ -1217,7 +1230,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                         *ab += 24 + 12;
                         ++bounces;
                         st |= kStCont;
-                        rays[(*nrays)++] = slot << 2 | kRayCont;
+                        rays->push(slot << 2 | kRayCont);
                     }
                 }
                 if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
@@ -1229,7 +1242,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
     store_s3(ps.L, N, slot, L);
     ps.st[slot] = st;
     *keep = (st & (kStCont | kStNee)) != 0;
-    *ab += 4 * (*nrays + (*keep ? 1u : 0u));  // ray / path queue entries written
+    *ab += 4 * (rays->n + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
 
 // Copy n 4-byte words global -> LDS, the whole block.
@@ -1265,7 +1278,10 @@ __device__ __forceinline__ DevScene stage_tables(const DevScene& sc, uint4* lds)
     return v;
 }
 
-template <int kFt, bool kTab>
+// kLean: the current path's body is loaded at the start of its own step
+// (ahead of the next path's head prefetch) instead of one path ahead -- the
+// register budget of 3 waves per SIMD for the kernels with the MIS branch.
+template <int kFt, bool kTab, bool kLean = false>
 __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
@@ -1287,8 +1303,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
     // experiment build: no prefetch (each path's loads, then its step)
     for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t rays[3];
-        uint32_t nrays = 0;
+        RayList rays;
         bool keep = false;
         uint32_t slot = 0;
         if (i < n) {
@@ -1298,11 +1313,40 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             path_prefetch_head(ps, slot, &pre);
             path_prefetch_body(ps, slot, &pre);
             path_load_now<kTab>(sc, ps, slot, pre, &now);
-            shade_path<kFt>(sc, hl, ps, slot, pre, now, rays, &nrays, &keep, &overflow, &ab);
+            shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
         }
-        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+        wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
     }
 #else
+    if constexpr (kLean) {
+        const uint32_t i0 = base + threadIdx.x;
+        uint32_t slot = 0, slot1 = 0;
+        PathPre pre{};  // this path's head (its body is loaded when its step starts)
+        if (i0 < n) {
+            slot = pq[i0];
+            path_prefetch_head(ps, slot, &pre);
+        }
+        if (i0 + stride < n) slot1 = pq[i0 + stride];
+        for (; base < n; base += stride) {
+            const uint32_t i = base + threadIdx.x;
+            PathPre nxt{};
+            PathNow now{};
+            uint32_t slot2 = 0;
+            if (i < n) {
+                path_prefetch_body(ps, slot, &pre);
+                path_load_now<kTab>(sc, ps, slot, pre, &now);
+            }
+            if (i + stride < n) path_prefetch_head(ps, slot1, &nxt);
+            if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
+            RayList rays;
+            bool keep = false;
+            if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
+            wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
+            slot = slot1;
+            slot1 = slot2;
+            pre = nxt;
+        }
+    } else {
     const uint32_t i0 = base + threadIdx.x;
     uint32_t slot = 0, slot1 = 0, slot2 = 0;
     PathPre pre{}, nxt{};  // this path (complete) and the next one (head only)
@@ -1325,16 +1369,16 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
         if (i + 2 * stride < n) path_prefetch_head(ps, slot2, &nn);
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
-        uint32_t rays[3];
-        uint32_t nrays = 0;
+        RayList rays;
         bool keep = false;
-        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, rays, &nrays, &keep, &overflow, &ab);
-        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
+        wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;
         slot1 = slot2;
         slot2 = slot3;
         pre = nxt;
         nxt = nn;
+    }
     }
 #endif
     wq_flush(wq, rq_out_count, rq_out, pq_out);
@@ -1358,8 +1402,8 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
 enum DlStep { kDlHit, kDlLights, kDlOne, kDlAcc, kDlSpecR, kDlSpecT, kDlReturn, kDlDone };
 
 template <int kFt>
-__device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t* rays,
-                                         uint32_t* nrays, bool* keep, bool* overflow) {
+__device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps, uint32_t slot, RayList* rays,
+                                         bool* keep, bool* overflow) {
     const uint32_t N = (uint32_t)ps.n;
     int* const I = ps.dli;
     float* const Fl = ps.dlf;
@@ -1371,7 +1415,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
     auto setf3 = [&](int k, S3 v) { Fl[k * N + slot] = v.c[0]; Fl[(k + 1) * N + slot] = v.c[1]; Fl[(k + 2) * N + slot] = v.c[2]; };
 
     uint32_t st = ps.st[slot];
-    *nrays = 0;
+    rays->n = 0;
     int d = I[kDlD * N + slot];
     Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
     int step;
@@ -1406,14 +1450,14 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
         vertex();
         if (sc.lights[PT_IDX(j, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
             if (portal_nee<kFt>(sc, ps, slot, j, si, bsdf, uS0, uS1)) {
-                rays[(*nrays)++] = slot << 2 | kRayA;
+                rays->push(slot << 2 | kRayA);
                 return true;
             }
             return false;
         }
         const uint32_t f = mis_nee<kFt>(sc, ps, slot, j, si, bsdf, uL0, uL1, uS0, uS1);
-        if (f & kNfA) rays[(*nrays)++] = slot << 2 | kRayShadow;
-        if (f & kNfB) rays[(*nrays)++] = slot << 2 | kRayB;
+        if (f & kNfA) rays->push(slot << 2 | kRayShadow);
+        if (f & kNfB) rays->push(slot << 2 | kRayB);
         return (f & (kNfA | kNfB)) != 0;
     };
     // Sampler::Get2DArray entry k of array ai: GetIndexForSample(s * n + k) (sampler.cpp:149-160)
@@ -1433,7 +1477,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
         ++d;
         haveV = false;
         st |= kStCont;
-        rays[(*nrays)++] = slot << 2 | kRayCont;
+        rays->push(slot << 2 | kRayCont);
     };
     bool emitted = false;
     while (!emitted && step != kDlDone) {
@@ -1458,7 +1502,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
                     const Ray r{offset_ray_origin(h.p, h.perr, h.n, ray.d), ray.d, kInf};
                     store_ray6(ps.ray, N, slot, r);
                     st |= kStCont;
-                    rays[(*nrays)++] = slot << 2 | kRayCont;
+                    rays->push(slot << 2 | kRayCont);
                     emitted = true;
                     break;
                 }
@@ -1609,15 +1653,14 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths 
     PT_WAVEQ(wq);
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t rays[3];
-        uint32_t nrays = 0;
+        RayList rays;
         bool keep = false;
         uint32_t slot = 0;
         if (i < n) {
             slot = pq[i];
-            shade_dl<kFt>(sc, ps, slot, rays, &nrays, &keep, &overflow);
+            shade_dl<kFt>(sc, ps, slot, &rays, &keep, &overflow);
         }
-        wq_push(wq, rays, nrays, keep, slot, rq_out_count, rq_out, pq_out);
+        wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
     }
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
@@ -1661,7 +1704,7 @@ __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, true>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, true, Ft<kFt>::mis>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;

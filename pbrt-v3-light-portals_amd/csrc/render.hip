@@ -1511,9 +1511,12 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) s->shade_variant = std::atoi(v);
-    else if (s->shade_tab && !s->hero) {
+    else if (s->shade_tab && !s->hero && s->features == kFtPortalOnly) {
         // the 3-waves-per-SIMD build of k_shade_tab when it needs no scratch (spills cost more than the
-        // third wave gains), with the grid-stride loop sized for it (PT_SHADE_BPC overrides)
+        // third wave gains), with the grid-stride loop sized for it (PT_SHADE_BPC overrides).  Only for
+        // portal-only scenes: the MIS kernels' 3-wave build gives up the body prefetch (kLean), and with
+        // two pipelines overlapping the 2-wave build, which leaves VGPRs for two trace waves per SIMD,
+        // renders C4 faster (442 vs 431 Msamples/s) although its isolated launches are slower
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, (const void*)shade_kernel(3, s->features)) == hipSuccess && fa.localSizeBytes == 0) {
             s->shade_variant = 3;

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Tests (unless SKIP_TESTS=1), then bench A/B over "config|ENV=.. ENV=.." items.
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest tests -q -m gpu -p no:cacheprovider --maxfail=5 --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+  case $rc in 0) ;; *) exit $rc;; esac
+fi
+i=0
+for item in "$@"; do
+  i=$((i+1))
+  cfg="${item%%|*}"; envs="${item#*|}"
+  env $envs timeout -k 10 400 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --config $cfg > gpurun_out/abc_$i.log 2>&1
+  rc=$?
+  echo "[$cfg $envs] rc=$rc $(python3 -c "
+import json
+d = json.loads(open('gpurun_out/abc_$i.log').read().strip().splitlines()[-1])
+k = d['roofline_kernels']
+print(d['value'], d['ms_per_step'], 'shade', k.get('k_shade', {}).get('avg_launch_ms'), 'trace', k['k_trace']['avg_launch_ms'])
+" 2>/dev/null)"
+  case $rc in 0) ;; *) exit $rc;; esac
+done
