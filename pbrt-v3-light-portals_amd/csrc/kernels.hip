@@ -682,6 +682,240 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
 #endif
 
 // ----------------------------------------------------------------------------
+// k_trace_lds: k_trace_nb for LDS-resident scenes with less work per node
+// visit.  The traversal kernel is VALU-issue-bound (C2: ~64 VALU per node
+// visit, about half of it bookkeeping around the box test), so:
+//  * node records are re-encoded while staged: word 1 .w = primitivesOffset +
+//    nPrimitives (the leaf's end) for a leaf, 0x80000000 | 1 << (16 + axis)
+//    for an interior node -- "interior?" is a sign test, "the ray runs against
+//    the split axis" one AND with the ray's direction sign bits (sgn); nodes
+//    are named by LDS byte address (word 1 .z of an interior node = its second
+//    child's), so the first child is +32 and a node load needs no address math;
+//  * the stack pointer is the LDS byte address of the top entry (row 0 of the
+//    lane's column is a dummy an empty stack's pop reads): a push writes 512
+//    bytes above it, a pop reads it, together with the node's two loads;
+//  * the slab updates are v_max / v_min (box_hit_mm).
+// Same visit order, tests, tMax updates and counters as k_trace_nb.
+// ----------------------------------------------------------------------------
+// Bounds3::IntersectP (geometry.h:1584-1606) with the reference's
+// compare-and-select slab updates as max / min: the same result whenever the
+// x-slab distances are numbers (with a y or z distance NaN, max / min keep the
+// other operand exactly as `if (tyMin > tMin) tMin = tyMin` does), and when an
+// x-slab distance is NaN the reference's test always fails (`NaN < tMax`,
+// `NaN > 0` are false), so that case is failed explicitly.  Signed zeros only
+// meet comparisons.
+__device__ __forceinline__ bool box_hit_mm(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2) {
+    const float kx = 1 + 2 * gammaf(3);
+    const float tx0 = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
+    float tx1 = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
+    const float ty0 = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
+    float ty1 = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
+    const float tz0 = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
+    float tz1 = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
+    tx1 *= kx;
+    ty1 *= kx;
+    tz1 *= kx;
+    const bool ok1 = !(tx0 > ty1) & !(ty0 > tx1);
+    const float m0 = __builtin_fmaxf(tx0, ty0);
+    const float m1 = __builtin_fminf(tx1, ty1);
+    const bool ok2 = !(m0 > tz1) & !(tz0 > m1);
+    const float f0 = __builtin_fmaxf(m0, tz0);
+    const float f1 = __builtin_fminf(m1, tz1);
+    return ok1 & ok2 & (f0 < ray.tmax) & (f1 > 0) & !__builtin_isunordered(tx0, tx1);
+}
+
+static_assert(kTraceBlock * 4 == 512, "k_trace_lds stack rows are 512 bytes apart");
+// 7 waves per SIMD (<= 72 VGPRs; the compiler's own choice lands at 74 = 6 waves)
+#ifdef PT_TRACE_WAVES
+#define PT_TRACE_LDS_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES)))
+#else
+#define PT_TRACE_LDS_ATTR __attribute__((amdgpu_waves_per_eu(kSph ? 1 : 7)))
+#endif
+// the node at LDS address addr (two ds_read_b128) and the stack's top entry, one wait
+__device__ __forceinline__ void lds_node_top(uint32_t addr, uint32_t sp, float4* a, float4* b, int* top) {
+    float4 x, y;
+    int t;
+    asm volatile(
+        "ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:16\n\tds_read_b32 %2, %4\n\ts_waitcnt lgkmcnt(0)"
+        : "=v"(x), "=v"(y), "=v"(t) : "v"(addr), "v"(sp) : "memory");
+    *a = x;
+    *b = y;
+    *top = t;
+}
+__device__ __forceinline__ void lds_push(uint32_t sp, int v) {
+    asm volatile("ds_write_b32 %0, %1 offset:512" : : "v"(sp), "v"(v) : "memory");
+}
+__device__ __forceinline__ int lds_top(uint32_t sp) {
+    int t;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(sp) : "memory");
+    return t;
+}
+
+template <bool kSph>
+__global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(DevScene sc, DevPaths ps,
+                                                                           const uint32_t* __restrict__ rq,
+                                                                           const uint32_t* __restrict__ rq_count,
+                                                                           uint32_t* fetch, int refill_min,
+                                                                           int leaf_min, DevStats* stats)
+#ifdef PT_TU_TRACE
+{
+    extern __shared__ float4 lds_dyn[];
+    const int nn = 2 * sc.n_nodes;
+    const int scene_f4 = nn + 3 * sc.n_prims;
+    const uint32_t node0 = (uint32_t)(uintptr_t)lds_dyn;  // nodes are named by their LDS byte address
+    for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
+        float4 v = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        if (i < nn && (i & 1)) {  // (offset, nPrimitives | axis << 16) -> the encoding above
+            const uint32_t npax = __float_as_uint(v.w);
+            const uint32_t np = npax & 0xffffu;
+            const uint32_t off = (uint32_t)__float_as_int(v.z);
+            v.w = __uint_as_float(np ? off + np : 0x80000000u | (1u << (16 + (npax >> 16))));
+            if (!np) v.z = __uint_as_float(node0 + 32u * off);  // second child: its LDS address
+        }
+        lds_dyn[i] = v;
+    }
+    __syncthreads();
+    const float4* bprims = lds_dyn + nn;
+    // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
+    const uint32_t sbase = (uint32_t)(uintptr_t)((int*)(lds_dyn + scene_f4) + threadIdx.x);
+    const uint32_t n = *rq_count;
+    const uint32_t N = (uint32_t)ps.n;
+    const uint32_t lane = lane_id();
+    uint32_t nrays = 0, nodes = 0, prims = 0;  // nrays: closest + shadow << 16
+    unsigned long long iters_w = 0;  // wave total
+    bool active = false, exhausted = false, drained = false;
+    uint32_t qn = 0, qe = 0;
+    uint32_t slot = 0, kind = 0;
+    Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
+    V3 inv = v3(0, 0, 0);
+    TriShear sh{0, 0, 0, 0};
+    bool n0 = false, n1 = false, n2 = false;
+    uint32_t sgn = 0, sp = sbase, cur = node0;
+    int hitPrim = -1, leafPos = 0, leafEnd = 0;
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
+                if (qn >= qe && !drained) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
+                    base = (uint32_t)__shfl((int)base, 0);
+                    qn = base < n ? base : n;
+                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
+                    drained = base + kTraceChunk >= n;
+                }
+                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
+                const uint32_t k = lanes_below(idle);
+                const uint32_t i = qn + k;
+                qn += take;
+                if (drained && qn >= qe) exhausted = true;
+                if (!active && k < take) {
+                    const uint32_t e = rq[i];
+                    slot = e >> 2;
+                    kind = e & 3u;
+                    const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
+                    ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
+                              v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
+                              kind == kRayShadow ? a[6 * N + slot] : kInf};
+                    inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                    sh = tri_shear(ray.d);
+                    n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
+                    sgn = (n0 ? 1u << 16 : 0u) | (n1 ? 1u << 17 : 0u) | (n2 ? 1u << 18 : 0u);
+                    cur = node0; sp = sbase; hitPrim = -1; leafPos = 0; leafEnd = 0;
+                    active = sc.n_nodes > 0;  // empty scene: every ray misses
+                    if (!active) {
+                        if (kind == kRayShadow) ps.hitA[slot] = 0;
+                        else if (kind == kRayCont) ps.hit[slot] = -1;
+                        else if (kind == kRayA) ps.hitA[slot] = -1;
+                        else ps.hitB[slot] = -1;
+                    }
+                    nrays += kind == kRayShadow ? 0x10000u : 1u;
+                }
+            }
+        }
+        const bool wantLeaf = active && leafPos < leafEnd;
+        const uint64_t mLeaf = __ballot(wantLeaf);
+        const uint64_t mNode = __ballot(active && !wantLeaf);
+        if ((mLeaf | mNode) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        ++iters_w;
+        bool done = false;
+        if (leafStep) {
+#pragma unroll
+            for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
+                if (!(active && !done && leafPos < leafEnd)) continue;
+                const int pi = leafPos++;
+                ++prims;
+                const float4 r0 = bprims[3 * pi];
+                const float4 r1 = bprims[3 * pi + 1];
+                const float4 r2 = bprims[3 * pi + 2];
+                const uint32_t fl = __float_as_uint(r0.w);
+                float t = 0;
+                bool ok;
+                if (fl & kPrimAnalytic) {
+                    ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
+                } else {
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
+                    ok &= (kind == kRayShadow) | !(fl & kPrimDegenerate);
+                }
+                hitPrim = ok ? pi : hitPrim;
+                ray.tmax = (ok && kind != kRayShadow) ? t : ray.tmax;
+                done = ok && kind == kRayShadow;
+                if (!done && leafPos == leafEnd) {  // the leaf is finished: pop
+                    const bool empty = sp == sbase;
+                    done = empty;
+                    if (!empty) {
+                        cur = (uint32_t)lds_top(sp);
+                        sp -= 512;
+                    }
+                }
+            }
+        } else {
+            // kNodeSteps node visits per loop iteration for lanes that stay in node mode
+#pragma unroll
+            for (int u = 0; u < kNodeSteps; ++u) {
+                if (!(active && !done && leafPos >= leafEnd)) continue;
+                ++nodes;
+                float4 a, b;
+                int top;
+                lds_node_top(cur, sp, &a, &b, &top);
+                const bool hit = box_hit_mm(a, b, ray, inv, n0, n1, n2);
+                const uint32_t off = __float_as_uint(b.z);  // leaf: primitivesOffset; interior: second child
+                const uint32_t w = __float_as_uint(b.w);
+                const bool inner = hit & ((int)w < 0);
+                const bool leaf = hit & ((int)w >= 0);
+                const bool neg = (w & sgn) != 0;
+                const bool empty = sp == sbase;
+                lds_push(sp, (int)(neg ? cur + 32u : off));  // the far child (kept only for an interior node)
+                done = !hit & empty;
+                const bool pop = !hit & !empty;
+                cur = inner ? (neg ? off : cur + 32u) : (pop ? (uint32_t)top : cur);
+                sp = inner ? sp + 512 : (pop ? sp - 512 : sp);
+                leafPos = leaf ? (int)off : leafPos;
+                leafEnd = leaf ? (int)w : leafEnd;
+            }
+        }
+        if (done) {
+            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
+            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
+            else ps.hitB[slot] = hitPrim;
+            active = false;
+        }
+    }
+    flush_stats(stats, nrays & 0xffffu, nrays >> 16, nodes, prims);
+    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
+}
+#else
+;
+#endif
+
+// ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
 // (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
 // ----------------------------------------------------------------------------

@@ -269,6 +269,7 @@ struct pt_scene {
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
+    bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
@@ -368,6 +369,7 @@ static TraceNbKernel trace_nb_kernel(bool lds, bool sph) {
     return lds ? (sph ? k_trace_nb<true, true> : k_trace_nb<true, false>)
                : (sph ? k_trace_nb<false, true> : k_trace_nb<false, false>);
 }
+static TraceNbKernel trace_lds_kernel(bool sph) { return sph ? k_trace_lds<true> : k_trace_lds<false>; }
 using TracePtKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, int*,
                                DevStats*);
 static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
@@ -1232,7 +1234,13 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     auto e = tev_new(false);
                     HIPCHK(hipEventRecord(e.first, st));
                     const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
-                    if (s->trace_persist == 2 && !s->trace_spill) {
+                    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
+                        // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
+                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+                        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
+                        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps,
+                                           rq_in, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+                    } else if (s->trace_persist == 2 && !s->trace_spill) {
                         // branch-reduced persistent traversal; LDS stack of depth+1 rows
                         const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
                         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
@@ -1525,6 +1533,13 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     }
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
+    if (const char* t = std::getenv("PT_TRACE_LEAN")) s->trace_lean = t[0] != '0';
+    if (std::getenv("PT_TRACE_DEBUG"))
+        std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,
+                     s->trace_spill, s->lds_scene_bytes,
+                     s->trace_persist == 2 && !s->trace_spill
+                         ? (s->lds_scene_bytes && s->trace_lean ? "k_trace_lds" : "k_trace_nb")
+                         : (s->trace_persist ? "k_trace_pt" : "k_trace"));
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
