@@ -453,6 +453,13 @@ pt_status pt_debug_camera_rays(pt_scene* scene, int n, const float* film_xy, flo
 /* BVH traversal for rays (o, d, tMax): closest primitive index in BVH order
  * (any = 0) or occlusion flag (any = 1); -1 for a miss. */
 pt_status pt_debug_trace(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim);
+/* The same queries through the traversal kernel pt_render runs for this scene
+ * (persistent, ray-queue driven, LDS-staged BVH when it fits): closest-hit rays
+ * take tMax = Infinity as the path tracer's do (rays7[6] is read for any = 1
+ * only).  counters (may be NULL): [0] BVH node visits, [1] primitive tests of
+ * the batch, the reference's BVHAccel counters (bvh.cpp:659-770). */
+pt_status pt_debug_trace_frame(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim,
+                               uint64_t* counters);
 /* BSDF::f / Pdf / Sample_f of scene material `material` in the local shading
  * frame (n = (0,0,1)): per record in8 = wo[3], wi[3], u0, u1 and
  * out8 = f[3], pdf, sampled wi[3], sampled pdf (f is the sampled f when wi

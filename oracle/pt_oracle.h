@@ -66,6 +66,8 @@ void oracle_set_trig(int correctly_rounded);
 int oracle_film_size(const pt_scene_desc* desc, int* w, int* h);
 float oracle_scrambled_radical_inverse_perm(int base_index, uint64_t a, const uint16_t* perm);
 int oracle_trace(const pt_scene_desc* desc, int n, const float* rays7, int any, int32_t* out);
+int oracle_trace_counted(const pt_scene_desc* desc, int n, const float* rays7, int any, int32_t* out,
+                         uint64_t* counts);
 
 /* Flattened BVH for comparison with the product's host BVH builder.
  * nodes: 8 x uint32 per node (32-byte LinearBVHNode image). */

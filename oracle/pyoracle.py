@@ -67,6 +67,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_ray_triangle.argtypes = [vp, vp, ctypes.c_float, vp, vp, vp, vp, vp]
         L.oracle_camera_ray.argtypes = [vp, ctypes.c_float, ctypes.c_float, vp, vp]
         L.oracle_trace.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
+        L.oracle_trace_counted.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         L.oracle_test_reintersect.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(ctypes.c_int)]
         L.oracle_test_triangle_sampling.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                     ctypes.POINTER(ctypes.c_double), vp, vp,
@@ -148,6 +149,16 @@ def trace(desc: int, rays7: np.ndarray, any_hit: bool) -> np.ndarray:
     out = np.zeros(len(rays7), np.int32)
     lib().oracle_trace(ctypes.c_void_p(desc), len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data)
     return out
+
+
+def trace_counted(desc: int, rays7: np.ndarray, any_hit: bool) -> Tuple[np.ndarray, int, int]:
+    """trace() plus the reference's BVH node-visit and primitive-test counts over the queries."""
+    rays7 = np.ascontiguousarray(rays7, np.float32)
+    out = np.zeros(len(rays7), np.int32)
+    counts = np.zeros(2, np.uint64)
+    _chk(lib().oracle_trace_counted(ctypes.c_void_p(desc), len(rays7), rays7.ctypes.data, int(any_hit),
+                                    out.ctypes.data, counts.ctypes.data))
+    return out, int(counts[0]), int(counts[1])
 
 
 def camera_ray(desc: int, fx: float, fy: float) -> Tuple[np.ndarray, np.ndarray]:

@@ -1061,6 +1061,39 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
     }
 }
 
+// One traversal launch over the nrays entries of ray queue rq (counts[0] holds
+// their number, counts[4] the persistent kernels' fetch cursor, zero): the
+// kernel this scene renders with (see create_scene_on).
+static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
+                         hipStream_t st) {
+    const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
+        // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
+        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
+        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
+                           counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+    } else if (s->trace_persist == 2 && !s->trace_spill) {
+        // branch-reduced persistent traversal; LDS stack of depth+1 rows
+        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
+        hipLaunchKernelGGL(trace_nb_kernel(s->lds_scene_bytes != 0, s->has_spheres), pg, dim3(kTraceBlock), lds, st,
+                           s->dev, ps, rq, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+    } else if (s->trace_persist) {
+        // persistent: about one resident wave set; lanes refill from counts[4]
+        auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
+        const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
+        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq, counts + 0, counts + 4, s->refill_min,
+                           s->leaf_min_pt, s->stack_rows, w.spill.p, w.stats.p);
+    } else {
+        const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * 16)));
+        if (s->lds_scene_bytes)
+            hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes, st,
+                               s->dev, ps, rq, counts + 0, w.spill.p, w.stats.p);
+        else
+            hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, st, s->dev, ps, rq,
+                               counts + 0, w.spill.p, w.stats.p);
+    }
+}
+
 __global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
     c[0] = rays;
     c[1] = paths;
@@ -1233,34 +1266,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 if (nrays > 0) {
                     auto e = tev_new(false);
                     HIPCHK(hipEventRecord(e.first, st));
-                    const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), maxBlocksTrace)));
-                    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
-                        // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
-                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-                        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
-                        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps,
-                                           rq_in, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
-                    } else if (s->trace_persist == 2 && !s->trace_spill) {
-                        // branch-reduced persistent traversal; LDS stack of depth+1 rows
-                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-                        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
-                        hipLaunchKernelGGL(trace_nb_kernel(s->lds_scene_bytes != 0, s->has_spheres), pg,
-                                           dim3(kTraceBlock), lds, st, s->dev, ps, rq_in, counts + 0, counts + 4,
-                                           s->refill_min, s->leaf_min, w.stats.p);
-                    } else if (s->trace_persist) {
-                        // persistent: about one resident wave set; lanes refill from counts[4]
-                        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-                        auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
-                        const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
-                        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq_in, counts + 0,
-                                           counts + 4, s->refill_min, s->leaf_min_pt, s->stack_rows, w.spill.p,
-                                           w.stats.p);
-                    } else if (s->lds_scene_bytes)
-                        hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes,
-                                           st, s->dev, ps, rq_in, counts + 0, w.spill.p, w.stats.p);
-                    else
-                        hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, st, s->dev,
-                                           ps, rq_in, counts + 0, w.spill.p, w.stats.p);
+                    launch_trace(s, w, ps, rq_in, counts, nrays, st);
                     HIPCHK(hipEventRecord(e.second, st));
                     pt[k].launches++;
                     sync_check("k_trace", iter);
@@ -2015,6 +2021,40 @@ pt_status pt_debug_trace(pt_scene* s, int n, const float* rays7, int any, int32_
                            any, sp.p, o.p);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpy(out_prim, o.p, sizeof(int) * n, hipMemcpyDeviceToHost));
+    });
+}
+
+pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, int32_t* out_prim,
+                               uint64_t* counters) {
+    return guarded([&] {
+        if (!s || n < 0 || (n && (!rays7 || !out_prim))) throw PtError(PT_ERR_INVALID_ARG, "null argument");
+        if (counters) counters[0] = counters[1] = 0;
+        if (n == 0) return;
+        HIPCHK(hipSetDevice(s->device));
+        Work w;
+        w.ensure((size_t)n, (size_t)s->num_cus * std::max(16, s->trace_bpc) * kTraceBlock, 0, 0);
+        DevPaths ps = w.paths(n);
+        const int nf = any ? 7 : 6;  // SoA: component c of ray i at c * n + i
+        std::vector<float> soa((size_t)nf * n);
+        std::vector<uint32_t> rq((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            for (int c = 0; c < nf; ++c) soa[(size_t)c * n + i] = rays7[7 * (size_t)i + c];
+            rq[i] = ((uint32_t)i << 2) | (any ? kRayShadow : kRayCont);
+        }
+        HIPCHK(hipMemcpy(any ? w.rayA.p : w.ray.p, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(w.rq0.p, rq.data(), rq.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(w.stats.p, 0, sizeof(DevStats)));
+        hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, 0, w.counts.p, (uint32_t)n, 0u);
+        launch_trace(s, w, ps, w.rq0.p, w.counts.p, (uint32_t)n, 0);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(out_prim, any ? w.hitA.p : w.hit.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+        if (counters) {
+            DevStats d;
+            HIPCHK(hipMemcpy(&d, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+            counters[0] = d.nodes;
+            counters[1] = d.prims;
+        }
     });
 }
 

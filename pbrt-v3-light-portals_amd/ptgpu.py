@@ -102,6 +102,7 @@ def lib() -> ctypes.CDLL:
     L.pt_debug_pixel_offsets.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_camera_rays.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_trace.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
+    L.pt_debug_trace_frame.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
     L.pt_debug_bsdf.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     _lib = L
     return L
@@ -410,6 +411,15 @@ class Scene:
         out = np.zeros(len(rays7), np.int32)
         _check(lib().pt_debug_trace(self._s, len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data))
         return out
+
+    def debug_trace_frame(self, rays7: np.ndarray, any_hit: bool) -> Tuple[np.ndarray, int, int]:
+        """The queries through the frame's traversal kernel: (hits, node visits, primitive tests)."""
+        rays7 = np.ascontiguousarray(rays7, np.float32)
+        out = np.zeros(len(rays7), np.int32)
+        cnt = np.zeros(2, np.uint64)
+        _check(lib().pt_debug_trace_frame(self._s, len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data,
+                                          cnt.ctypes.data))
+        return out, int(cnt[0]), int(cnt[1])
 
     def debug_bsdf(self, material: int, rec8: np.ndarray) -> np.ndarray:
         """(n, 8) records wo, wi, u0, u1 -> (n, 8) f, pdf, sampled wi, sampled pdf."""

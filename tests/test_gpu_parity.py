@@ -99,6 +99,55 @@ def test_traversal_bit_exact(variant, any_hit):
     assert np.array_equal(got, ref)
 
 
+def _edge_rays(sc, n_rand, n_edge, seed, tmax):
+    """Random rays plus the slab test's edge cases (Bounds3::IntersectP,
+    geometry.h:1584-1606): direction components +0 / -0 (inverse direction
+    +inf / -inf) from origins lying exactly on BVH node bounds, where the
+    reference's slab distances are 0 * inf = NaN."""
+    nodes, _ = sc.bvh()
+    b = np.ascontiguousarray(nodes[:, :6]).view(np.float32)  # bmin xyz, bmax xyz
+    rng = np.random.default_rng(seed)
+    axis_dirs = np.array([(1, 0, 0), (0, 1, 0), (0, 0, 1), (0.6, 0.8, 0), (0, 0.6, 0.8), (0.8, 0, 0.6)], np.float32)
+    edge = np.zeros((n_edge, 7), np.float32)
+    for k in range(n_edge):
+        lo, hi = b[rng.integers(len(b))].reshape(2, 3)
+        o = rng.uniform(lo - 5, hi + 5).astype(np.float32)
+        on = rng.random(3) < 0.7  # coordinates put exactly on a bound of the node
+        o = np.where(on, np.where(rng.random(3) < 0.5, lo, hi), o)
+        d = axis_dirs[rng.integers(len(axis_dirs))] * np.where(rng.random(3) < 0.5, -1, 1).astype(np.float32)
+        edge[k, :3], edge[k, 3:6], edge[k, 6] = o, d, tmax  # zero components keep their random sign
+    return np.concatenate([_random_rays(n_rand, seed, tmax), edge]).astype(np.float32)
+
+
+TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
+    "k_trace_lds": {},
+    "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
+    "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
+    "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
+    "k_trace_pt_spill": {"PT_TRACE_PERSIST": "1", "PT_STACK_ROWS": "2", "PT_TRACE_LDS": "0"},
+    "k_trace": {"PT_TRACE_PERSIST": "0"},
+}
+
+
+@pytest.mark.parametrize("kernel", sorted(TRACE_KERNELS))
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_frame_traversal_kernels_bit_exact(variant, monkeypatch, kernel, any_hit):
+    """Every traversal kernel pt_render can run, on random and slab-edge-case
+    rays: the hit primitive (closest) or occlusion flag (any-hit) and the
+    reference's node-visit / primitive-test counters equal the oracle's."""
+    for k, v in TRACE_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+    hs, sc = _scene(variant(**MINI))
+    rays = _edge_rays(sc, 6000, 6000, 5, np.inf if not any_hit else 300.0)
+    _, order = sc.bvh()
+    got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
+    ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
+    if not any_hit:
+        got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
+    assert np.array_equal(got, ref)
+    assert (nodes, prims) == (rnodes, rprims)
+
+
 def test_bvh_device_matches_oracle(variant):
     hs, sc = _scene(variant(**MINI))
     n1, o1 = sc.bvh()
