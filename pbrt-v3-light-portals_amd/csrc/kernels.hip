@@ -697,13 +697,19 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
 //  * the slab updates are v_max / v_min (box_hit_mm).
 // Same visit order, tests, tMax updates and counters as k_trace_nb.
 // ----------------------------------------------------------------------------
-// Bounds3::IntersectP (geometry.h:1584-1606) with the reference's
-// compare-and-select slab updates as max / min: the same result whenever the
-// x-slab distances are numbers (with a y or z distance NaN, max / min keep the
-// other operand exactly as `if (tyMin > tMin) tMin = tyMin` does), and when an
-// x-slab distance is NaN the reference's test always fails (`NaN < tMax`,
-// `NaN > 0` are false), so that case is failed explicitly.  Signed zeros only
-// meet comparisons.
+// Bounds3::IntersectP (geometry.h:1584-1606) as max3 / min3 of the slab
+// distances.  The reference's sequence -- reject if tMin > tyMax or tyMin >
+// tMax, tMin = max, tMax = min, the same with z, then tMin < ray.tMax and
+// tMax > 0 -- gives the same answer:
+//  * with every distance a number, its two rejections are the six cross-axis
+//    pairs of max(t0) <= min(t1); the three same-axis pairs t0 <= t1 can only
+//    fail when that axis' far distance u is negative (t1 = u * gamma-scale <=
+//    u), and then tMax <= t1 < 0 fails `tMax > 0` anyway;
+//  * a NaN y / z distance constrains nothing there (its comparisons are false,
+//    `if (tyMin > tMin)` keeps tMin) and max / min skip it the same way;
+//  * a NaN x distance leaves the reference's tMin or tMax NaN to the end,
+//    where `NaN < tMax` / `NaN > 0` fail: failed explicitly here.
+// Signed zeros only meet comparisons.
 __device__ __forceinline__ bool box_hit_mm(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2) {
     const float kx = 1 + 2 * gammaf(3);
     const float tx0 = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
@@ -715,13 +721,9 @@ __device__ __forceinline__ bool box_hit_mm(float4 a, float4 b, const Ray& ray, V
     tx1 *= kx;
     ty1 *= kx;
     tz1 *= kx;
-    const bool ok1 = !(tx0 > ty1) & !(ty0 > tx1);
-    const float m0 = __builtin_fmaxf(tx0, ty0);
-    const float m1 = __builtin_fminf(tx1, ty1);
-    const bool ok2 = !(m0 > tz1) & !(tz0 > m1);
-    const float f0 = __builtin_fmaxf(m0, tz0);
-    const float f1 = __builtin_fminf(m1, tz1);
-    return ok1 & ok2 & (f0 < ray.tmax) & (f1 > 0) & !__builtin_isunordered(tx0, tx1);
+    const float f0 = __builtin_fmaxf(__builtin_fmaxf(tx0, ty0), tz0);
+    const float f1 = __builtin_fminf(__builtin_fminf(tx1, ty1), tz1);
+    return !(f0 > f1) & (f0 < ray.tmax) & (f1 > 0) & !__builtin_isunordered(tx0, tx1);
 }
 
 static_assert(kTraceBlock * 4 == 512, "k_trace_lds stack rows are 512 bytes apart");
