@@ -1010,6 +1010,244 @@ __global__ __launch_bounds__(256) void k_film_s60(DevHero h, DevPaths ps, FilmCo
 ;
 #endif
 
+// k_film_s60 with the source samples staged through LDS.  k_film_s60 reads a
+// sample's 240-B radiance once for every film pixel its filter footprint
+// reaches (~16 with the 2-pixel Gaussian) and at 128 spp those re-reads miss
+// L2 (29 GB per launch against ~2 GB of samples).  Here a block owns an 8x8
+// square of film pixels (16 waves, each wave 2x2 of them, lane = bin as in
+// k_film_s60) and streams the source pixels its filter windows reach through
+// LDS, 128 samples at a time, double-buffered (one barrier per chunk): each
+// sample is read from HBM once per block, (8 + 2 win)^2 / 64 times in all.
+// Every film pixel still consumes the stream in its own order -- FilmTile by
+// FilmTile (tile row, tile column), source pixels in scan order, samples in
+// order -- because the block's stream is that order over the union of the
+// windows and a film pixel skips what lies outside its own; the per-bin sums,
+// the ToXYZ per FilmTile and the merges are k_film_s60's operations in
+// k_film_s60's order (bit-identical films).
+constexpr int kF60Ch = 128;      // samples per staged chunk
+constexpr int kF60MaxWin = 5;    // larger filter windows take k_film_s60
+constexpr int kF60List = (8 + 2 * kF60MaxWin) * (8 + 2 * kF60MaxWin);
+__global__ __launch_bounds__(1024) void k_film_s60_blk(DevHero h, DevPaths ps, FilmConsts fc,
+                                                       const int* __restrict__ pixslot, int p0, int np, int nsamp,
+                                                       int bx0, int by0, int bw, int bh, float4* accum)
+#ifdef PT_TU_HERO
+{
+    __shared__ float4 s_v[2][kF60Ch * kNS / 4];  // the chunk's 60-bin radiances, slot-major
+    __shared__ float4 s_m[2][kF60Ch];            // dx, dy, sanitiser factor k
+    __shared__ int4 s_b[2][kF60Ch];              // the sample's pixel bounds x0, x1, y0, y1 (AddSample)
+    __shared__ int s_lp[kF60List], s_lq[kF60List];  // stream: batch pixel, (qy - sb_y0) << 16 | (qx - sb_x0)
+    __shared__ float s_tab[256];
+    __shared__ int s_n;
+    const int tid = (int)threadIdx.x, lane = (int)lane_id();
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nbx = (bw + 7) >> 3;
+    const int gx0 = bx0 + ((int)blockIdx.x % nbx) * 8, gy0 = by0 + ((int)blockIdx.x / nbx) * 8;
+    const int gx1 = min(gx0 + 7, bx0 + bw - 1), gy1 = min(gy0 + 7, by0 + bh - 1);
+    const int rx0 = max(gx0 - fc.win, fc.sb_x0), rx1 = min(gx1 + fc.win, fc.sb_x1 - 1);
+    const int ry0 = max(gy0 - fc.win, fc.sb_y0), ry1 = min(gy1 + fc.win, fc.sb_y1 - 1);
+    const int sbw = fc.sb_x1 - fc.sb_x0;
+    if (tid < 256) s_tab[tid] = fc.table[tid];
+    // the stream: source pixels of this batch inside the region, FilmTile by
+    // FilmTile, scan order within a tile (wave 0, ballot-compacted)
+    if (wid == 0) {
+        int n = 0;
+        if (rx0 <= rx1 && ry0 <= ry1) {
+            for (int tr = (ry0 - fc.sb_y0) >> 4; tr <= (ry1 - fc.sb_y0) >> 4; ++tr) {
+                for (int tc = (rx0 - fc.sb_x0) >> 4; tc <= (rx1 - fc.sb_x0) >> 4; ++tc) {
+                    const int qy0 = max(ry0, fc.sb_y0 + 16 * tr), qy1 = min(ry1, fc.sb_y0 + 16 * tr + 15);
+                    const int qx0 = max(rx0, fc.sb_x0 + 16 * tc), qx1 = min(rx1, fc.sb_x0 + 16 * tc + 15);
+                    const int rw = qx1 - qx0 + 1, cnt = rw * (qy1 - qy0 + 1);
+                    for (int b = 0; b < cnt; b += 64) {
+                        const int k = b + lane;
+                        int p = -1, qy = 0, qx = 0;
+                        if (k < cnt) {
+                            qy = qy0 + k / rw;
+                            qx = qx0 + k % rw;
+                            p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
+                        }
+                        const bool ok = p >= 0 && p < np;
+                        const uint64_t m = __ballot(ok);
+                        if (ok) {
+                            const int at = n + (int)lanes_below(m);
+                            s_lp[at] = p;
+                            s_lq[at] = ((qy - fc.sb_y0) << 16) | (qx - fc.sb_x0);  // sb may start below 0
+                        }
+                        n += __popcll(m);
+                    }
+                }
+            }
+        }
+        if (lane == 0) s_n = n;
+    }
+    // this wave's film pixels: 2x2, wave (w & 3, w >> 2) of the 4x4 grid of pairs
+    int tx[4], ty[4], wx0[4], wx1[4], wy0[4], wy1[4];
+    bool on[4], any[4] = {false, false, false, false}, touched[4] = {false, false, false, false};
+    float binsum[4] = {0.f, 0.f, 0.f, 0.f}, wsum[4] = {0.f, 0.f, 0.f, 0.f};
+    float4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        tx[j] = gx0 + 2 * (wid & 3) + (j & 1);
+        ty[j] = gy0 + 2 * (wid >> 2) + (j >> 1);
+        wy0[j] = max(ty[j] - fc.win, fc.sb_y0), wy1[j] = min(ty[j] + fc.win, fc.sb_y1 - 1);
+        wx0[j] = max(tx[j] - fc.win, fc.sb_x0), wx1[j] = min(tx[j] + fc.win, fc.sb_x1 - 1);
+        on[j] = tx[j] <= gx1 && ty[j] <= gy1 && wy0[j] <= wy1[j] && wx0[j] <= wx1[j];
+        acc[j] = on[j] ? accum[(size_t)(ty[j] - fc.crop_y0) * (fc.crop_x1 - fc.crop_x0) + (tx[j] - fc.crop_x0)]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int n = s_n;
+    const int nch = (nsamp + kF60Ch - 1) / kF60Ch;
+    const int total = n * nch;
+    // staging registers: two float4 of radiance and (threads < 128) one sample's metadata
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, rm = r0;
+    int4 rb = make_int4(0, 0, 0, 0);
+    auto stage_load = [&](int e) {
+        const int i = e / nch, c = e - i * nch;
+        const int cnt = min(kF60Ch, nsamp - c * kF60Ch);
+        const size_t s0 = (size_t)s_lp[i] * (size_t)nsamp + (size_t)c * kF60Ch;
+        const float4* src = reinterpret_cast<const float4*>(h.out60 + s0 * kNS);
+        const int nf = cnt * (kNS / 4);
+        if (tid < nf) r0 = src[tid];
+        if (tid + 1024 < nf) r1 = src[tid + 1024];
+        if (tid < cnt) {
+            const uint32_t slot = (uint32_t)(s0 + tid);
+            const float2 pf = ps.pfilm[slot];
+            const float dx = pf.x - 0.5f, dy = pf.y - 0.5f;
+            rb = make_int4((int)ceilf(dx - fc.rx), (int)floorf(dx + fc.rx) + 1, (int)ceilf(dy - fc.ry),
+                           (int)floorf(dy + fc.ry) + 1);
+            // radiance sanitiser (hero.cpp:118-140) and maxSampleLuminance
+            const float yv = h.out_y[slot];  // -inf: a NaN bin
+            float k;
+            if ((double)yv < -1e-5 || __builtin_isinf(yv)) k = 0.f;
+            else if (yv > fc.max_lum) k = fc.max_lum / yv;
+            else k = 1.f;
+            rm = make_float4(dx, dy, k, 0.f);
+        }
+    };
+    auto stage_store = [&](int e, int b) {
+        const int i = e / nch, c = e - i * nch;
+        const int cnt = min(kF60Ch, nsamp - c * kF60Ch);
+        const int nf = cnt * (kNS / 4);
+        if (tid < nf) s_v[b][tid] = r0;
+        if (tid + 1024 < nf) s_v[b][tid + 1024] = r1;
+        if (tid < cnt) {
+            s_m[b][tid] = rm;
+            s_b[b][tid] = rb;
+        }
+    };
+    // ToXYZ of a film pixel's FilmTile contribSum, merged (k_film_s60's order)
+    auto close_tile = [&](int j) {
+        if (any[j]) {
+            float x = 0.f, y = 0.f, z = 0.f;
+            for (int i = 0; i < kNS; ++i) {
+                const float c = lane_val(binsum[j], i);
+                x += h.XYZ[i] * c;
+                y += h.XYZ[kNS + i] * c;
+                z += h.XYZ[2 * kNS + i] * c;
+            }
+            const float scale = (float)(700 - 400) / (float)(106.856895f * kNS);
+            acc[j].x += x * scale;
+            acc[j].y += y * scale;
+            acc[j].z += z * scale;
+            acc[j].w += wsum[j];
+            touched[j] = true;
+        }
+        binsum[j] = 0.f;
+        wsum[j] = 0.f;
+        any[j] = false;
+    };
+    if (total > 0) {
+        stage_load(0);
+        stage_store(0, 0);
+    }
+    __syncthreads();
+    int cur_tile = -1;
+    for (int e = 0; e < total; ++e) {
+        const int b = e & 1;
+        if (e + 1 < total) stage_load(e + 1);
+        const int i = e / nch, c = e - i * nch;
+        const int cnt = min(kF60Ch, nsamp - c * kF60Ch);
+        const int q = s_lq[i];
+        const int qy = (q >> 16) + fc.sb_y0, qx = (q & 0xffff) + fc.sb_x0;
+        const int tile = ((q >> 20) << 16) | ((q & 0xffff) >> 4);
+        if (tile != cur_tile) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) close_tile(j);
+            cur_tile = tile;
+        }
+        bool need = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            need |= on[j] && qx >= wx0[j] && qx <= wx1[j] && qy >= wy0[j] && qy <= wy1[j];
+        if (need) {
+            float4 mh[2];
+            int4 bh2[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int sl = hh * 64 + lane;
+                mh[hh] = sl < cnt ? s_m[b][sl] : make_float4(0.f, 0.f, 0.f, 0.f);
+                bh2[hh] = sl < cnt ? s_b[b][sl] : make_int4(1, 0, 1, 0);  // empty bounds: no touch
+            }
+            const float* sv = reinterpret_cast<const float*>(&s_v[b][0]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!(on[j] && qx >= wx0[j] && qx <= wx1[j] && qy >= wy0[j] && qy <= wy1[j])) continue;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    if (hh * 64 >= cnt) break;
+                    const int4 bb = bh2[hh];
+                    const bool touch = !(tx[j] < bb.x || tx[j] >= bb.y || ty[j] < bb.z || ty[j] >= bb.w);
+                    float w = 0.f;
+                    if (touch) {
+                        const float dx = mh[hh].x, dy = mh[hh].y;
+                        const float fxv = fabsf((tx[j] - dx) * fc.inv_rx * 16);
+                        const float fyv = fabsf((ty[j] - dy) * fc.inv_ry * 16);
+                        int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                        int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                        w = s_tab[iy * 16 + ix];
+                    }
+                    const float k = mh[hh].z;
+                    uint64_t m = __ballot(touch);
+                    if (m) any[j] = true;
+                    while (m) {
+                        int js[4];
+                        float vs[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            js[u] = m ? __ffsll((unsigned long long)m) - 1 : -1;
+                            m &= m - 1;
+                            vs[u] = (js[u] >= 0 && lane < kNS) ? sv[(hh * 64 + js[u]) * kNS + lane] : 0.f;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (js[u] < 0) break;
+                            const float kj = lane_val(k, js[u]), wj = lane_val(w, js[u]);
+                            if (lane < kNS) {
+                                float v = vs[u];
+                                if (kj == 0.f) v = 0.f;        // L = Spectrum(0.f)
+                                else if (kj != 1.f) v = v * kj;  // L *= maxSampleLuminance / L.y()
+                                binsum[j] += (v * 1.f) * wj;
+                            }
+                            wsum[j] += wj;
+                        }
+                    }
+                }
+            }
+        }
+        if (e + 1 < total) stage_store(e + 1, b ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        close_tile(j);
+        if (touched[j] && lane == 0)
+            accum[(size_t)(ty[j] - fc.crop_y0) * (fc.crop_x1 - fc.crop_x0) + (tx[j] - fc.crop_x0)] = acc[j];
+    }
+}
+#else
+;
+#endif
+
 // SpatialLightDistribution::ComputeDistribution (lightdistrib.cpp:175-236)
 // for every voxel: 128 radical-inverse points, each light's Li.y() / pdf,
 // floored at 0.001 x the average, as a Distribution1D (sampling.h:65-88).

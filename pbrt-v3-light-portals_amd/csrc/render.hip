@@ -186,7 +186,8 @@ struct Work {
     void ensure(size_t n, size_t spill_threads, int frames, int hero_slots) {
         if (!host_counts) {
             void* p = nullptr;
-            if (hipHostMalloc(&p, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            // written by k_next_counts at the end of each bounce (system-coherent, no copy engine or blit)
+            if (hipHostMalloc(&p, 8 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
                 throw PtError(PT_ERR_OOM, "hipHostMalloc failed");
             host_counts = (uint32_t*)p;
         }
@@ -272,6 +273,7 @@ struct pt_scene {
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
+    int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
     int leaf_min_pt = 16;        // k_trace_pt (HBM-resident BVHs): the same threshold
@@ -1094,6 +1096,23 @@ static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_
     }
 }
 
+// End of a bounce: the output queue sizes become the next bounce's input sizes,
+// and go to the host's pinned words directly.  A hipMemcpyAsync here ran as a
+// 1024-thread blit kernel that waited (up to 9 ms, C2 kernel trace) for a CU
+// with room beside the other pipeline's persistent trace blocks; one lane
+// fits anywhere.
+__global__ void k_next_counts(uint32_t* c, volatile uint32_t* host) {
+    const uint32_t rays = c[2], paths = c[3];
+    host[0] = rays;
+    host[1] = paths;
+    c[0] = rays;
+    c[1] = paths;
+    c[2] = 0;
+    c[3] = 0;
+    c[4] = 0;
+    c[5] = 0;
+}
+
 __global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
     c[0] = rays;
     c[1] = paths;
@@ -1289,11 +1308,11 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 HIPCHK(hipEventRecord(es.second, st));
                 pt[k].shade_launches++;
                 sync_check("k_shade", iter);
-                HIPCHK(hipMemcpyAsync(w.host_counts, counts + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                hipLaunchKernelGGL(k_next_counts, dim3(1), dim3(1), 0, st, counts, w.host_counts);
+                HIPCHK(hipGetLastError());
                 HIPCHK(hipStreamSynchronize(st));
-                nrays = w.host_counts[0];
-                npaths = w.host_counts[1];
-                hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, st, counts, nrays, npaths);
+                nrays = ((volatile uint32_t*)w.host_counts)[0];
+                npaths = ((volatile uint32_t*)w.host_counts)[1];
                 std::swap(rq_in, rq_out);
                 std::swap(pq_in, pq_out);
                 if (++iter > 100000) throw PtError(PT_ERR_STATE, "path loop did not terminate");
@@ -1307,7 +1326,10 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
             if (bw > 0 && bh > 0) {
                 const dim3 fg(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32)));
-                if (s->hero)
+                if (s->hero && s->film_blk && s->film.win <= kF60MaxWin)
+                    hipLaunchKernelGGL(k_film_s60_blk, dim3(ceil_div(bw, 8) * ceil_div(bh, 8)), dim3(1024), 0, st, hh,
+                                       ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);
+                else if (s->hero)
                     hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, st, hh, ps, s->film, dslot.p, g.p0, g.np,
                                        ns, g.bx0, g.by0, bw, bh, d_accum);
                 else
@@ -1546,6 +1568,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                      s->trace_persist == 2 && !s->trace_spill
                          ? (s->lds_scene_bytes && s->trace_lean ? "k_trace_lds" : "k_trace_nb")
                          : (s->trace_persist ? "k_trace_pt" : "k_trace"));
+    if (const char* t = std::getenv("PT_FILM_BLK")) s->film_blk = std::atoi(t);
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));

@@ -266,3 +266,36 @@ def test_hero_furnace_matches_oracle(tmp_path, integrator):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("filt,spp", [("gaussian2", 136), ("box", 70), ("gaussian3", 20), ("gaussian6", 6)])
+def test_hero_film_staged_matches_oracle(tmp_path, filt, spp):
+    """The 60-bin film under a crop window and batches of two FilmTiles, with
+    the box filter's 1-pixel window and Gaussian windows of 3, 4 and 7 pixels
+    == the oracle, bit for bit; and the opt-in LDS-staged k_film_s60_blk
+    (PT_FILM_BLK=1: several 128-sample chunks per source pixel at 136 spp, a
+    partial chunk at 70 spp; a window above kF60MaxWin, gaussian radius 6,
+    falls back to k_film_s60) gives the identical film."""
+    txt = open(_c3_variant(tmp_path, "hero_path_mis", res=24, spp=spp)).read()
+    txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [37]', txt)
+    txt = txt.replace('Film "image"', 'Film "image" "float cropwindow" [0.05 0.93 0.1 0.85]')
+    if filt == "box":
+        txt = re.sub(r'PixelFilter "gaussian"\s*"float xwidth" \[2\]\s*"float ywidth" \[2\]', 'PixelFilter "box"', txt)
+    else:
+        r = filt[len("gaussian"):]
+        txt = re.sub(r'"float ([xy])width" \[2\]', r'"float \1width" [%s]' % r, txt)
+    p = tmp_path / f"c3_film_{filt}.pbrt"
+    p.write_text(txt)
+    hs = ptgpu.HostScene(str(p))
+    ref, _ = pyoracle.render(hs.desc, nthreads=8)
+    slots = 16 * 16 * spp * 2  # two FilmTiles per batch
+    got, _ = ptgpu.Scene(hs, batch_slots=slots).render()
+    assert ref.mean() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    os.environ["PT_FILM_BLK"] = "1"
+    try:
+        staged, _ = ptgpu.Scene(hs, batch_slots=slots).render()
+    finally:
+        del os.environ["PT_FILM_BLK"]
+    assert np.array_equal(staged.view(np.uint32), got.view(np.uint32))
