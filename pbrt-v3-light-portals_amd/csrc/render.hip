@@ -212,7 +212,7 @@ struct Work {
             rayB.alloc(6 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
             cap = n;
         }
-        spill.alloc(spill_threads * 64);
+        spill.alloc(spill_threads * kCbSpillWords);  // k_trace_pt uses 64 words per lane, k_trace_cb 128
         counts.alloc(8);
         stats.alloc(1);
     }
@@ -232,7 +232,7 @@ struct Work {
 }  // namespace pt
 
 struct pt_scene {
-    pt::DBuf<float4> nodes, prims;
+    pt::DBuf<float4> nodes, prims, crec;
     pt::DBuf<pt_triangle> tris;
     pt::DBuf<float> P, N, S, UV, lfunc, lcdf, tri_area, perm_c0;
     pt::DBuf<pt::DevPlane> planes, pplanes;
@@ -270,6 +270,9 @@ struct pt_scene {
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
+    bool trace_cb = false;       // HBM-resident BVH under trace_persist 2: k_trace_cb (child-pair records; opt-in PT_TRACE_CB=1)
+    int cb_rows = 0;             // k_trace_cb: LDS stack rows (<= kCbStackRows), deeper entries spill
+    bool cb_spill = false;
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
@@ -383,6 +386,10 @@ static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
     return sph ? k_trace_pt<false, false, true> : k_trace_pt<false, false, false>;
 }
 using TraceKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, int*, DevStats*);
+static TracePtKernel trace_cb_kernel(bool spill, bool sph) {
+    if (spill) return sph ? k_trace_cb<true, true> : k_trace_cb<true, false>;
+    return sph ? k_trace_cb<false, true> : k_trace_cb<false, false>;
+}
 static TraceKernel trace_kernel(bool lds, bool sph) {
     return lds ? (sph ? k_trace<true, true> : k_trace<true, false>) : (sph ? k_trace<false, true> : k_trace<false, false>);
 }
@@ -1074,6 +1081,11 @@ static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
         hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
                            counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+    } else if (s->trace_persist == 2 && s->trace_cb) {
+        // child-pair records from HBM: LDS stack rows of references + entry distances
+        const size_t lds = (size_t)2 * s->cb_rows * kTraceBlock * sizeof(int);
+        hipLaunchKernelGGL(trace_cb_kernel(s->cb_spill, s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
+                           counts + 0, counts + 4, s->refill_min, s->leaf_min_pt, s->cb_rows, w.spill.p, w.stats.p);
     } else if (s->trace_persist == 2 && !s->trace_spill) {
         // branch-reduced persistent traversal; LDS stack of depth+1 rows
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
@@ -1544,6 +1556,39 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     const char* e = std::getenv("PT_TRACE_LDS");
     s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                              ? scene_bytes : 0;
+    {   // child-pair records for an HBM-resident BVH (k_trace_cb), unless a leaf does not fit the encoding
+        const char* c = std::getenv("PT_TRACE_CB");
+        s->cb_rows = std::min(s->stack_rows, kCbStackRows);
+        s->cb_spill = sbound > s->cb_rows;
+        // opt-in (PT_TRACE_CB=1): C5 traces slower with it
+        s->trace_cb = s->lds_scene_bytes == 0 && !s->host_nodes.empty() && c && c[0] == '1' &&
+                      sbound <= s->cb_rows + kCbSpillWords / 2;
+        const auto& hn = s->host_nodes;
+        auto ref_of = [&](size_t c) -> int {
+            const LinearNode& m = hn[c];
+            if (m.nprims == 0) return (int)c;
+            if (m.nprims > 127 || m.offset < 0 || m.offset >= (1 << 24)) s->trace_cb = false;
+            return (int)(0x80000000u | (uint32_t)m.nprims << 24 | (uint32_t)m.offset);
+        };
+        if (s->trace_cb) {
+            std::vector<float4> rec(4 * hn.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+            for (size_t i = 0; i < hn.size() && s->trace_cb; ++i) {
+                if (hn[i].nprims > 0) continue;
+                const size_t a = i + 1, b = (size_t)hn[i].offset;
+                const LinearNode &A = hn[a], &B = hn[b];
+                rec[4 * i] = make_float4(A.bmin[0], A.bmin[1], A.bmin[2], A.bmax[0]);
+                rec[4 * i + 1] = make_float4(A.bmax[1], A.bmax[2], __builtin_bit_cast(float, ref_of(a)),
+                                             __builtin_bit_cast(float, ref_of(b)));
+                rec[4 * i + 2] = make_float4(B.bmin[0], B.bmin[1], B.bmin[2], B.bmax[0]);
+                rec[4 * i + 3] = make_float4(B.bmax[1], B.bmax[2], __builtin_bit_cast(float, (int)hn[i].axis), 0.f);
+            }
+            s->dev.cb_root = ref_of(0);
+            if (s->trace_cb) {
+                s->crec.upload(rec);
+                s->dev.crec = s->crec.p;
+            }
+        }
+    }
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) s->shade_variant = std::atoi(v);
@@ -1565,9 +1610,11 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (std::getenv("PT_TRACE_DEBUG"))
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,
                      s->trace_spill, s->lds_scene_bytes,
-                     s->trace_persist == 2 && !s->trace_spill
-                         ? (s->lds_scene_bytes && s->trace_lean ? "k_trace_lds" : "k_trace_nb")
-                         : (s->trace_persist ? "k_trace_pt" : "k_trace"));
+                     s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean ? "k_trace_lds"
+                     : s->trace_persist == 2 && s->trace_cb                                        ? "k_trace_cb"
+                     : s->trace_persist == 2 && !s->trace_spill                                    ? "k_trace_nb"
+                     : s->trace_persist                                                            ? "k_trace_pt"
+                                                                                                   : "k_trace");
     if (const char* t = std::getenv("PT_FILM_BLK")) s->film_blk = std::atoi(t);
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));

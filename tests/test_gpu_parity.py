@@ -123,6 +123,8 @@ TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders 
     "k_trace_lds": {},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
+    "k_trace_cb": {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1"},
+    "k_trace_cb_spill": {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1", "PT_STACK_ROWS": "2"},
     "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
     "k_trace_pt_spill": {"PT_TRACE_PERSIST": "1", "PT_STACK_ROWS": "2", "PT_TRACE_LDS": "0"},
     "k_trace": {"PT_TRACE_PERSIST": "0"},
@@ -240,7 +242,9 @@ def test_tile_groups_batching_equal(variant):
 
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}])
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"},
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1"},
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1", "PT_STACK_ROWS": "3"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
