@@ -177,11 +177,11 @@ struct DevPaths {
     float* beta;        // 3n
     float* eta;         // n
     uint32_t* st;       // n: packed state, see kSt* below
-    float* ray;         // 6n continuation ray o,d
+    float* ray;         // 8n continuation ray: 32-B record per slot {o.xyz, d.x} {d.yz, tMax, 0} (kernels.hip load_ray)
     int* hit;           // n
-    float* rayA;        // 7n NEE ray A o,d,tMax
+    float* rayA;        // 8n NEE ray A (MIS shadow ray: its tMax), same record
     int* hitA;          // n
-    float* rayB;        // 6n NEE ray B o,d
+    float* rayB;        // 8n NEE ray B, same record
     int* hitB;          // n
     float* nee;         // kNee * n payload
     // DirectLightingIntegrator only (null otherwise): see kDl* below

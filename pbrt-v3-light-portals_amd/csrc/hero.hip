@@ -530,7 +530,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     float etaScale = H[kHsEtaScale * BS], bsdfPdf = H[kHsBsdfPdf * BS];
     bool isWvlDependent = (hf & kHfWvlDep) != 0;
     const bool isLastSpecular = (hf & kHfLastSpec) != 0;
-    Ray ray = load_ray6(ps.ray, N, slot, kInf);
+    Ray ray = load_ray(ps.ray, slot, kInf);
     sb += 4 + 56 + 24 + 4;  // hidx, H wavelengths / pdfs / etaScale / bsdfPdf, ray, hit
     const V3 rayO = ray.o;
     const int hpr = ps.hit[slot];
@@ -596,7 +596,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
         const pt_material& M = sc.mats[PT_IDX(mat, sc.n_mats)];
         if (bounces >= sc.max_depth) {
         } else if (M.kind == PT_MAT_NONE) {  // bounces-- ; continue
-            store_ray6(ps.ray, N, slot, Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf});
+            store_ray(ps.ray, slot, Ray{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf});
             sb += 24;
             rays->push(slot << 2 | kRayCont);
             cont = true;
@@ -644,10 +644,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         const V3 origin = offset_ray_origin(si.p, si.perr, si.n, sp - si.p);
                         const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
                         const V3 dd = target - origin;
-                        float* a = ps.rayA;
-                        a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
-                        a[3 * N + slot] = dd.x; a[4 * N + slot] = dd.y; a[5 * N + slot] = dd.z;
-                        a[6 * N + slot] = 1 - kShadowEps;
+                        store_ray(ps.rayA, slot, Ray{origin, dd, 1 - kShadowEps});
                         sb += 28;
                         rays->push(slot << 2 | kRayShadow);
                         st |= kStNee;
@@ -826,7 +823,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
                         isWvlDependent |= curWvlDep;
                         hf = (hf & ~(kHfWvlDep | kHfLastSpec)) | (isWvlDependent ? kHfWvlDep : 0u) |
                              ((flags & kBxSpecular) ? kHfLastSpec : 0u);
-                        store_ray6(ps.ray, N, slot, ray);
+                        store_ray(ps.ray, slot, ray);
                         sb += 24 + 40;  // ray; H pdfs / etaScale / bsdfPdf
                         rays->push(slot << 2 | kRayCont);
                         cont = true;

@@ -224,12 +224,33 @@ __device__ __forceinline__ int traverse(const DevScene& sc, const float4* __rest
     return hitPrim;
 }
 
-__device__ __forceinline__ Ray load_ray6(const float* a, uint32_t n, uint32_t slot, float tmax) {
-    return Ray{v3(a[slot], a[n + slot], a[2 * n + slot]), v3(a[3 * n + slot], a[4 * n + slot], a[5 * n + slot]), tmax};
+// Ray records (DevPaths::ray / rayA / rayB): 32 B per slot, {o.xyz, d.x} {d.yz, tMax, 0} -- one
+// 32-B sector, two 16-B accesses per lane (round 2's SoA fields took six or seven 4-B accesses, each
+// its own sector when a queue's slots are spread).  tMax is the shadow ray's bound (ray A of the MIS
+// estimator), kInf for closest-hit rays.
+__device__ __forceinline__ Ray load_ray(const float* a, uint32_t slot) {
+    const float4* r = reinterpret_cast<const float4*>(a) + 2 * (size_t)slot;
+    const float4 p = r[0], q = r[1];
+    return Ray{v3(p.x, p.y, p.z), v3(p.w, q.x, q.y), q.z};
 }
-__device__ __forceinline__ void store_ray6(float* a, uint32_t n, uint32_t slot, const Ray& r) {
-    a[slot] = r.o.x; a[n + slot] = r.o.y; a[2 * n + slot] = r.o.z;
-    a[3 * n + slot] = r.d.x; a[4 * n + slot] = r.d.y; a[5 * n + slot] = r.d.z;
+__device__ __forceinline__ Ray load_ray(const float* a, uint32_t slot, float tmax) {
+    Ray r = load_ray(a, slot);
+    r.tmax = tmax;
+    return r;
+}
+// the traversal's refill: o, d and (shadow rays only) tMax -- one 16-B, one 8-B and one 4-B load,
+// no register for the record's pad word
+__device__ __forceinline__ Ray load_ray_trace(const float* a, uint32_t slot, bool shadow) {
+    const float4* r = reinterpret_cast<const float4*>(a) + 2 * (size_t)slot;
+    const float4 p = r[0];
+    const float2 q = *reinterpret_cast<const float2*>(r + 1);
+    const float t = shadow ? reinterpret_cast<const float*>(r + 1)[2] : kInf;
+    return Ray{v3(p.x, p.y, p.z), v3(p.w, q.x, q.y), t};
+}
+__device__ __forceinline__ void store_ray(float* a, uint32_t slot, const Ray& r) {
+    float4* d = reinterpret_cast<float4*>(a) + 2 * (size_t)slot;
+    d[0] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    d[1] = make_float4(r.d.y, r.d.z, r.tmax, 0.f);
 }
 
 // kLdsScene: small scenes (nodes + prim records <= kLdsSceneMax bytes) are
@@ -253,7 +274,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
         bprims = lds_scene + nn;
     }
     const uint32_t n = *rq_count;
-    const uint32_t N = (uint32_t)ps.n;
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
     int* myspill = spill + (size_t)gtid * (64 - kStackLds);
     unsigned long long nodes = 0, prims = 0, ncl = 0, nsh = 0;
@@ -261,17 +281,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
         const uint32_t e = rq[i];
         const uint32_t slot = e >> 2, kind = e & 3u;
         if (kind == kRayShadow) {
-            const float* a = ps.rayA;
-            Ray r{v3(a[slot], a[N + slot], a[2 * N + slot]), v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
-                  a[6 * N + slot]};
+            Ray r = load_ray(ps.rayA, slot);
             int h = traverse<true, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             ps.hitA[slot] = h >= 0 ? 1 : 0;
             ++nsh;
         } else {
             Ray r;
-            if (kind == kRayCont) r = load_ray6(ps.ray, N, slot, kInf);
-            else if (kind == kRayA) r = load_ray6(ps.rayA, N, slot, kInf);
-            else r = load_ray6(ps.rayB, N, slot, kInf);
+            if (kind == kRayCont) r = load_ray(ps.ray, slot, kInf);
+            else if (kind == kRayA) r = load_ray(ps.rayA, slot, kInf);
+            else r = load_ray(ps.rayB, slot, kInf);
             int h = traverse<false, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
             if (kind == kRayCont) ps.hit[slot] = h;
             else if (kind == kRayA) ps.hitA[slot] = h;
@@ -345,7 +363,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
     }
     int* stk = (int*)(lds_dyn + scene_f4);  // [row][kTraceBlock]
     const uint32_t n = *rq_count;
-    const uint32_t N = (uint32_t)ps.n;
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
@@ -381,10 +398,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                         const uint32_t e = rq[i];
                         slot = e >> 2;
                         kind = e & 3u;
-                        const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
-                        ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
-                                  v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
-                                  kind == kRayShadow ? a[6 * N + slot] : kInf};
+                        ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                         sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
@@ -558,7 +572,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_CB_ATTR void k_trace_cb(DevSc
     const float4* __restrict__ rec = sc.crec;
     const float4* __restrict__ bprims = sc.prims;
     const uint32_t n = *rq_count;
-    const uint32_t N = (uint32_t)ps.n;
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * kCbSpillWords;
@@ -605,10 +618,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_CB_ATTR void k_trace_cb(DevSc
                         const uint32_t e = rq[i];
                         slot = e >> 2;
                         kind = e & 3u;
-                        const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
-                        ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
-                                  v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
-                                  kind == kRayShadow ? a[6 * N + slot] : kInf};
+                        ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                         sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
@@ -761,7 +771,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
     }
     int* stk = (int*)(lds_dyn + scene_f4) + threadIdx.x;  // entry k at stk[k * kTraceBlock]
     const uint32_t n = *rq_count;
-    const uint32_t N = (uint32_t)ps.n;
     const uint32_t lane = lane_id();
     uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
     bool active = false, exhausted = false, drained = false;
@@ -798,10 +807,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
                         const uint32_t e = rq[i];
                         slot = e >> 2;
                         kind = e & 3u;
-                        const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
-                        ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
-                                  v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
-                                  kind == kRayShadow ? a[6 * N + slot] : kInf};
+                        ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                         sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
@@ -1004,7 +1010,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
     // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
     const uint32_t sbase = (uint32_t)(uintptr_t)((int*)(lds_dyn + scene_f4) + threadIdx.x);
     const uint32_t n = *rq_count;
-    const uint32_t N = (uint32_t)ps.n;
     const uint32_t lane = lane_id();
     uint32_t nrays = 0, nodes = 0, prims = 0;  // nrays: closest + shadow << 16
     unsigned long long iters_w = 0;  // wave total
@@ -1039,10 +1044,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                     const uint32_t e = rq[i];
                     slot = e >> 2;
                     kind = e & 3u;
-                    const float* a = kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA);
-                    ray = Ray{v3(a[slot], a[N + slot], a[2 * N + slot]),
-                              v3(a[3 * N + slot], a[4 * N + slot], a[5 * N + slot]),
-                              kind == kRayShadow ? a[6 * N + slot] : kInf};
+                    ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
                     inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                     sh = tri_shear(ray.d);
                     n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
@@ -1191,7 +1193,7 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
             ps.dli[kDlS * N + slot] = s0 + (int)sl;
             ps.dli[kDlPix * N + slot] = (int)off;
         }
-        store_ray6(ps.ray, N, slot, r);
+        store_ray(ps.ray, slot, r);
         rq[slot] = slot << 2 | kRayCont;
         pq[slot] = slot;
     }
@@ -1282,12 +1284,12 @@ __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uin
         in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
     if (portalA) in.pdf = nee[kNeePdf * N + slot];
     if ((fl & kNfPortal) && (fl & kNfDivPortal)) in.w = nee[kNeePortalPdf * N + slot];
-    if (portalA && hA >= 0) in.ray = load_ray6(ps.rayA, N, slot, kInf);
+    if (portalA && hA >= 0) in.ray = load_ray(ps.rayA, slot, kInf);
     if (misB) {
         in.nl = __float_as_int(nee[kNeeLight * N + slot]);
         in.w = nee[kNeeSw * N + slot];
         in.pdf = nee[kNeeSpdf * N + slot];
-        in.ray = load_ray6(ps.rayB, N, slot, kInf);
+        in.ray = load_ray(ps.rayB, slot, kInf);
     }
     return in;
 }
@@ -1295,8 +1297,6 @@ __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uin
 template <int kFt>
 __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
                                         int hA, int hB, const NeeIn& in) {
-    const uint32_t N = (uint32_t)ps.n;
-    const float* nee = ps.nee;
     S3 Ld = s3(0.f);
     if (fl & kNfPortal) {
         if (fl & kNfA) {
@@ -1360,7 +1360,6 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                                            uint32_t* ab = nullptr) {
     const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
     const DevPlane& lp = sc.planes[PT_IDX(l.shape, sc.n_planes)];
-    const uint32_t N = (uint32_t)ps.n;
     uint32_t flags = kNfPortal;
     if (l.strategy != PT_PORTAL_LIGHT) {
         const V3 pObj = xf_point(lp.w2o, it.p);
@@ -1432,7 +1431,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                 }
                 if (pdf > 0) {
                     const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
-                    store_ray6(ps.rayA, N, slot, r);
+                    store_ray(ps.rayA, slot, r);
                     put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
                     put_nee(ps, slot, kNeePdf, pdf);
                     put_nee3(ps, slot, kNeeLi, s3(0.f));
@@ -1451,7 +1450,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
     const S3 Li = area_sample_li<kFt>(sc, l, it, u10, u11, &wi, &pdf, &sp, &sn, &spe);
     if (!is_black(Li) && pdf > 0) {
         const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
-        store_ray6(ps.rayA, N, slot, r);
+        store_ray(ps.rayA, slot, r);
         put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
         put_nee(ps, slot, kNeePdf, pdf);
         put_nee3(ps, slot, kNeeLi, Li);
@@ -1470,7 +1469,6 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
                                             const SurfHit& it, const Bsdf& bsdf, float ul0, float ul1, float us0,
                                             float us1, uint32_t* ab = nullptr) {
     const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
-    const uint32_t N = (uint32_t)ps.n;
     uint32_t flags = kNfMis;
     V3 wi, sp, sn, spe;
     float lightPdf = 0, scatteringPdf = 0;
@@ -1483,10 +1481,7 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
             const V3 origin = offset_ray_origin(it.p, it.perr, it.n, sp - it.p);
             const V3 target = offset_ray_origin(sp, spe, sn, origin - sp);
             const V3 d = target - origin;
-            float* a = ps.rayA;
-            a[slot] = origin.x; a[N + slot] = origin.y; a[2 * N + slot] = origin.z;
-            a[3 * N + slot] = d.x; a[4 * N + slot] = d.y; a[5 * N + slot] = d.z;
-            a[6 * N + slot] = 1 - kShadowEps;
+            store_ray(ps.rayA, slot, Ray{origin, d, 1 - kShadowEps});
             if (l.kind == PT_LIGHT_POINT) {  // IsDeltaLight: no MIS weight (integrator.cpp:186-188)
                 put_nee3(ps, slot, kNeeF, (f * Li) / lightPdf);
             } else {
@@ -1508,7 +1503,7 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
             if (lp != 0) {
                 const float sw = power_heuristic(pdf2, lp);
                 const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi2), wi2, kInf};
-                store_ray6(ps.rayB, N, slot, r);
+                store_ray(ps.rayB, slot, r);
                 put_nee3(ps, slot, kNeeLi, f);
                 put_nee(ps, slot, kNeeSw, sw);
                 put_nee(ps, slot, kNeeSpdf, pdf2);
@@ -1566,7 +1561,7 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
     if (p->st & kStCont) {
         p->hidx = ps.hidx[slot];
         p->beta = load_s3(ps.beta, N, slot);
-        p->ray = load_ray6(ps.ray, N, slot, kInf);
+        p->ray = load_ray(ps.ray, slot, kInf);
         p->eta = ps.eta[slot];
     }
 }
@@ -1622,7 +1617,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
             if (sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_NONE) {
                 // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
                 const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
-                store_ray6(ps.ray, N, slot, r);
+                store_ray(ps.ray, slot, r);
                 *ab += 24;
                 st |= kStCont;
                 rays->push(slot << 2 | kRayCont);
@@ -1698,7 +1693,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                         else beta = beta / (1 - q);
                     }
                     if (alive) {
-                        store_ray6(ps.ray, N, slot, r);
+                        store_ray(ps.ray, slot, r);
                         store_s3(ps.beta, N, slot, beta);
                         *ab += 24 + 12;
                         ++bounces;
@@ -1946,7 +1941,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
         fr(d, kFrPdf) = pdf;
         fr(d, kFrPhase) = __int_as_float(phase);
         const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};  // SpawnRay
-        store_ray6(ps.ray, N, slot, r);
+        store_ray(ps.ray, slot, r);
         ++d;
         haveV = false;
         st |= kStCont;
@@ -1956,7 +1951,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
     while (!emitted && step != kDlDone) {
         switch (step) {
             case kDlHit: {
-                const Ray ray = load_ray6(ps.ray, N, slot, kInf);
+                const Ray ray = load_ray(ps.ray, slot, kInf);
                 const int hp = ps.hit[slot];
                 SurfHit h;
                 const bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &h);
@@ -1973,7 +1968,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
                 prim_info<Ft<kFt>::sph>(sc, hp, &mat, &light);
                 if (sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_NONE) {  // Li(isect.SpawnRay(ray.d), depth)
                     const Ray r{offset_ray_origin(h.p, h.perr, h.n, ray.d), ray.d, kInf};
-                    store_ray6(ps.ray, N, slot, r);
+                    store_ray(ps.ray, slot, r);
                     st |= kStCont;
                     rays->push(slot << 2 | kRayCont);
                     emitted = true;

@@ -208,8 +208,8 @@ struct Work {
         }
         if (n > cap) {
             hidx.alloc(n); st.alloc(n); rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
-            pfilm.alloc(n); L.alloc(3 * n); beta.alloc(3 * n); eta.alloc(n); ray.alloc(6 * n); rayA.alloc(7 * n);
-            rayB.alloc(6 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
+            pfilm.alloc(n); L.alloc(3 * n); beta.alloc(3 * n); eta.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
+            rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
             cap = n;
         }
         spill.alloc(spill_threads * kCbSpillWords);  // k_trace_pt uses 64 words per lane, k_trace_cb 128
@@ -2104,11 +2104,11 @@ pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, 
         Work w;
         w.ensure((size_t)n, (size_t)s->num_cus * std::max(16, s->trace_bpc) * kTraceBlock, 0, 0);
         DevPaths ps = w.paths(n);
-        const int nf = any ? 7 : 6;  // SoA: component c of ray i at c * n + i
-        std::vector<float> soa((size_t)nf * n);
+        // ray records (kernels.hip load_ray): {o.xyz, d.x} {d.yz, tMax, 0}
+        std::vector<float> soa((size_t)8 * n, 0.f);
         std::vector<uint32_t> rq((size_t)n);
         for (int i = 0; i < n; ++i) {
-            for (int c = 0; c < nf; ++c) soa[(size_t)c * n + i] = rays7[7 * (size_t)i + c];
+            for (int c = 0; c < 7; ++c) soa[(size_t)8 * i + c] = rays7[7 * (size_t)i + c];
             rq[i] = ((uint32_t)i << 2) | (any ? kRayShadow : kRayCont);
         }
         HIPCHK(hipMemcpy(any ? w.rayA.p : w.ray.p, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
