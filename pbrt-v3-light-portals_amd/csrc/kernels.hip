@@ -2283,6 +2283,122 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
 ;
 #endif
 
+// k_film_t: k_film with lane = film pixel.  k_film gives a film pixel one wave
+// (lane = sample) and folds the touching samples into its FilmTile sums one
+// readlane at a time: a serial chain of dependent adds per pixel, ~16 K long
+// at 1024 spp with the 2-pixel Gaussian (C3: 20.9 ms per launch).  Here a wave
+// owns an 8 x 8 square of film pixels and walks the source pixels their filter
+// windows reach -- FilmTile by FilmTile (tile row, tile column), scan order
+// within a tile, samples in order -- 64 samples at a time: lane j loads sample
+// j, applies the sanitiser and maxSampleLuminance (film.h AddSample's caller,
+// integrator.cpp:568-600) and finds its pixel bounds, then the samples that
+// reach the square are broadcast one by one and every lane adds the ones
+// touching its pixel.  Each film pixel sees its samples in k_film's order and
+// does k_film's operations, so the sums are bit-identical; the 64 pixels'
+// chains run side by side.
+__global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
+                                                int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum)
+#ifdef PT_TU_MISC
+{
+    __shared__ float s_tab[256];
+    if (threadIdx.x < 256) s_tab[threadIdx.x] = fc.table[threadIdx.x];
+    __syncthreads();
+    const uint32_t N = (uint32_t)ps.n;
+    const int cw = fc.crop_x1 - fc.crop_x0;
+    const int sbw = fc.sb_x1 - fc.sb_x0;
+    const int lane = (int)lane_id();
+    const int nbx = (bw + 7) >> 3, nsq = nbx * ((bh + 7) >> 3);
+    const int sq = (int)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (sq >= nsq) return;
+    const int gx0 = bx0 + (sq % nbx) * 8, gy0 = by0 + (sq / nbx) * 8;
+    const int gx1 = min(gx0 + 7, bx0 + bw - 1), gy1 = min(gy0 + 7, by0 + bh - 1);
+    const int tx = gx0 + (lane & 7), ty = gy0 + (lane >> 3);
+    const bool on = tx <= gx1 && ty <= gy1 && max(ty - fc.win, fc.sb_y0) <= min(ty + fc.win, fc.sb_y1 - 1) &&
+                    max(tx - fc.win, fc.sb_x0) <= min(tx + fc.win, fc.sb_x1 - 1);
+    const size_t o = (size_t)(ty - fc.crop_y0) * cw + (tx - fc.crop_x0);
+    float4 acc = on ? accum[o] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool touched = false;
+    const int rx0 = max(gx0 - fc.win, fc.sb_x0), rx1 = min(gx1 + fc.win, fc.sb_x1 - 1);
+    const int ry0 = max(gy0 - fc.win, fc.sb_y0), ry1 = min(gy1 + fc.win, fc.sb_y1 - 1);
+    if (rx0 <= rx1 && ry0 <= ry1) {
+        for (int tr = (ry0 - fc.sb_y0) >> 4; tr <= (ry1 - fc.sb_y0) >> 4; ++tr) {
+            for (int tc = (rx0 - fc.sb_x0) >> 4; tc <= (rx1 - fc.sb_x0) >> 4; ++tc) {
+                const int qy0 = max(ry0, fc.sb_y0 + 16 * tr), qy1 = min(ry1, fc.sb_y0 + 16 * tr + 15);
+                const int qx0 = max(rx0, fc.sb_x0 + 16 * tc), qx1 = min(rx1, fc.sb_x0 + 16 * tc + 15);
+                float p0s = 0.f, p1s = 0.f, p2s = 0.f, wsum = 0.f;  // this pixel's FilmTile contribSum
+                bool any = false;
+                for (int qy = qy0; qy <= qy1; ++qy) {
+                    for (int qx = qx0; qx <= qx1; ++qx) {
+                        const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
+                        if (p < 0 || p >= np) continue;
+                        for (int c0 = 0; c0 < nsamp; c0 += 64) {
+                            const int sl = c0 + lane;
+                            // lane = sample sl: bounds, sanitised radiance, and whether it reaches the square
+                            float dx = 0.f, dy = 0.f;
+                            S3 L = s3(0.f);
+                            int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+                            bool reach = false;
+                            if (sl < nsamp) {
+                                const uint32_t slot = (uint32_t)p * (uint32_t)nsamp + (uint32_t)sl;
+                                const float2 pf = ps.pfilm[slot];
+                                dx = pf.x - 0.5f;
+                                dy = pf.y - 0.5f;
+                                x0 = (int)ceilf(dx - fc.rx); x1 = (int)floorf(dx + fc.rx) + 1;
+                                y0 = (int)ceilf(dy - fc.ry); y1 = (int)floorf(dy + fc.ry) + 1;
+                                reach = !(gx1 < x0 || gx0 >= x1 || gy1 < y0 || gy0 >= y1);
+                                if (reach) {
+                                    L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                                    if (has_nan(L)) L = s3(0.f);
+                                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
+                                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
+                                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                                }
+                            }
+                            // the bounds relative to the square's corner, one byte each (|offset| <= 8 + win)
+                            const uint32_t bb = (uint32_t)(uint8_t)(x0 - gx0 + 64) | (uint32_t)(uint8_t)(x1 - gx0 + 64) << 8 |
+                                                (uint32_t)(uint8_t)(y0 - gy0 + 64) << 16 | (uint32_t)(uint8_t)(y1 - gy0 + 64) << 24;
+                            uint64_t m = __ballot(reach);
+                            const int lx = (lane & 7) + 64, ly = (lane >> 3) + 64;
+                            while (m) {
+                                const int j = __ffsll((unsigned long long)m) - 1;
+                                m &= m - 1;
+                                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bb, j);
+                                const bool touch = on && !(lx < (int)(b & 255u) || lx >= (int)((b >> 8) & 255u) ||
+                                                           ly < (int)((b >> 16) & 255u) || ly >= (int)(b >> 24));
+                                if (touch) {
+                                    const float sdx = lane_val(dx, j), sdy = lane_val(dy, j);
+                                    const float fxv = fabsf((tx - sdx) * fc.inv_rx * 16);
+                                    const float fyv = fabsf((ty - sdy) * fc.inv_ry * 16);
+                                    int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                                    int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                                    const float w = s_tab[iy * 16 + ix];
+                                    const S3 c = (s3(lane_val(L.c[0], j), lane_val(L.c[1], j), lane_val(L.c[2], j)) * 1.f) * w;
+                                    p0s += c.c[0];
+                                    p1s += c.c[1];
+                                    p2s += c.c[2];
+                                    wsum += w;
+                                    any = true;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (!any) continue;
+                // RGBSpectrum::ToXYZ (spectrum.h:64-68) of the tile pixel, merged
+                acc.x += 0.412453f * p0s + 0.357580f * p1s + 0.180423f * p2s;
+                acc.y += 0.212671f * p0s + 0.715160f * p1s + 0.072169f * p2s;
+                acc.z += 0.019334f * p0s + 0.119193f * p1s + 0.950227f * p2s;
+                acc.w += wsum;
+                touched = true;
+            }
+        }
+    }
+    if (touched) accum[o] = acc;
+}
+#else
+;
+#endif
+
 // ----------------------------------------------------------------------------
 // Test hooks (parity unit tests through the C ABI)
 // ----------------------------------------------------------------------------

@@ -276,6 +276,7 @@ struct pt_scene {
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
+    int film_t = 1;              // RGB film, filter windows of 2-16 pixels: k_film_t (lane = film pixel; PT_FILM_T=0: k_film)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
@@ -1344,6 +1345,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 else if (s->hero)
                     hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, st, hh, ps, s->film, dslot.p, g.p0, g.np,
                                        ns, g.bx0, g.by0, bw, bh, d_accum);
+                else if (s->film_t && s->film.win >= 2 && s->film.win <= 16)  // box (win 1): k_film is faster
+                    hipLaunchKernelGGL(k_film_t, dim3(ceil_div(ceil_div(bw, 8) * ceil_div(bh, 8), 4)), dim3(256), 0, st, ps,
+                                       s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);
                 else
                     hipLaunchKernelGGL(k_film, fg, dim3(256), 0, st, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0,
                                        g.by0, bw, bh, d_accum);
@@ -1616,6 +1620,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                      : s->trace_persist                                                            ? "k_trace_pt"
                                                                                                    : "k_trace");
     if (const char* t = std::getenv("PT_FILM_BLK")) s->film_blk = std::atoi(t);
+    if (const char* t = std::getenv("PT_FILM_T")) s->film_t = std::atoi(t);
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));

@@ -641,3 +641,32 @@ def test_lamp_matches_oracle(tmp_path, integrator, strategy):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+@pytest.mark.parametrize("filt,spp", [("gaussian", 70), ("box", 9), ("gaussian3", 5)])
+def test_film_pixel_lanes_match_oracle(tmp_path, monkeypatch, filt, spp):
+    """k_film_t (the RGB film with one lane per film pixel, 8x8 pixels per
+    wave; filter windows of 2-16 pixels): the 2-pixel Gaussian of config 3 at
+    70 spp (two 64-sample chunks per source pixel) and a 3-pixel Gaussian,
+    plus the box filter (k_film), under a crop window with an odd film size
+    and batches of two FilmTiles == the oracle's film bit for bit, and ==
+    k_film (PT_FILM_T=0)."""
+    import re
+    from conftest import scene_variant
+    path = scene_variant(tmp_path, name="cornell_dielectric.pbrt", res=(45, 38), spp=spp)
+    txt = open(path).read().replace('Film "image"', 'Film "image" "float cropwindow" [0.07 0.95 0.12 0.9]')
+    if filt == "box":
+        txt = re.sub(r'PixelFilter "gaussian"\s*"float xwidth" \[2\]\s*"float ywidth" \[2\]', 'PixelFilter "box"', txt)
+    elif filt == "gaussian3":
+        txt = re.sub(r'"float ([xy])width" \[2\]', r'"float \1width" [3]', txt)
+    p = tmp_path / f"film_{filt}.pbrt"
+    p.write_text(txt)
+    hs = ptgpu.HostScene(str(p))
+    slots = 16 * 16 * spp * 2
+    got, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
+    ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
+    assert ref[..., 3].max() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    monkeypatch.setenv("PT_FILM_T", "0")
+    old, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
+    assert np.array_equal(old.view(np.uint32), got.view(np.uint32))
