@@ -50,6 +50,26 @@ def test_replicas_match_single_device(tmp_path, ndev):
     _close(many, one)
 
 
+def _gpus() -> int:
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_gpus() < 2, reason="needs two GPUs (the test box has one)")
+def test_replicas_on_distinct_devices(tmp_path):
+    """Replicas on two different devices: the films cross devices by
+    hipMemcpyPeer and are summed on ids[0]; each replica's streams and
+    buffers are freed with its own device current.  Same frame as one device."""
+    import ptgpu
+    hs = ptgpu.HostScene(scene_variant(tmp_path, res=(72, 40), spp=8))
+    one, st1 = ptgpu.Scene(hs, device=0).render()
+    sc = ptgpu.Scene(hs, devices=[0, 1])
+    many, stn = sc.render()
+    del sc
+    _same_counts(st1, stn)
+    _close(many, one)
+
+
 def test_replicas_take_batch_and_pipeline_settings(tmp_path):
     """pt_set_batch_slots / pt_set_pipelines reach every replica (the query
     reads -1 when a replica differs); a small batch on two replicas renders
