@@ -276,7 +276,7 @@ struct pt_scene {
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
-    int film_t = 1;              // RGB film, filter windows of 2-16 pixels: k_film_t (lane = film pixel; PT_FILM_T=0: k_film)
+    int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
@@ -886,7 +886,17 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     fc.sb_x0 = fr.sb_x0; fc.sb_y0 = fr.sb_y0; fc.sb_x1 = fr.sb_x1; fc.sb_y1 = fr.sb_y1;
     fc.rx = rx; fc.ry = ry;
     fc.inv_rx = 1 / rx; fc.inv_ry = 1 / ry;
-    fc.win = (int)std::ceil(std::max(rx, ry) + 0.5f);
+    {   // source pixels whose samples can reach a film pixel t: a sample of pixel q has pFilm in [q, q + 1]
+        // (the pixel plus a [0, 1) offset, rounded), so AddSample's bounds (film.h:121-161) give
+        // ceil(q + f - 0.5 - r) <= t <= floor(q + f - 0.5 + r), i.e. |q - t| <= floor(0.5 + r) -- with a
+        // margin of floor(0.5 + r) + 0.5 - r on both sides, which float rounding cannot cross unless it is
+        // tiny (then one more pixel).  Round 2 used ceil(r + 0.5): 7 x 7 source pixels for the
+        // 2-pixel Gaussian instead of 5 x 5.
+        const float r = std::max(rx, ry);
+        int w = (int)std::floor(0.5f + r);
+        if ((float)w + 0.5f - r < 1e-3f) w += 1;
+        fc.win = w;
+    }
     fc.max_lum = f.max_sample_luminance;
     {
         float expX = 0, expY = 0, alpha = f.gaussian_alpha;

@@ -645,8 +645,8 @@ def test_lamp_matches_oracle(tmp_path, integrator, strategy):
 
 @pytest.mark.parametrize("filt,spp", [("gaussian", 70), ("box", 9), ("gaussian3", 5)])
 def test_film_pixel_lanes_match_oracle(tmp_path, monkeypatch, filt, spp):
-    """k_film_t (the RGB film with one lane per film pixel, 8x8 pixels per
-    wave; filter windows of 2-16 pixels): the 2-pixel Gaussian of config 3 at
+    """k_film_t (opt-in PT_FILM_T=1: the RGB film with one lane per film
+    pixel, 8x8 pixels per wave; filter windows of 2-16 pixels): the 2-pixel Gaussian of config 3 at
     70 spp (two 64-sample chunks per source pixel) and a 3-pixel Gaussian,
     plus the box filter (k_film), under a crop window with an odd film size
     and batches of two FilmTiles == the oracle's film bit for bit, and ==
@@ -663,6 +663,7 @@ def test_film_pixel_lanes_match_oracle(tmp_path, monkeypatch, filt, spp):
     p.write_text(txt)
     hs = ptgpu.HostScene(str(p))
     slots = 16 * 16 * spp * 2
+    monkeypatch.setenv("PT_FILM_T", "1")
     got, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
     ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
     assert ref[..., 3].max() > 0
