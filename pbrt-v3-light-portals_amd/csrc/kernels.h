@@ -23,7 +23,7 @@ constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kCbSpillWords = 128;  // k_trace_cb: global spill per lane, two words per entry
 constexpr int kCbStackRows = kStackLds;  // k_trace_cb LDS stack rows (x2 words: 20 KB per block, 4 waves per SIMD)
 constexpr int kShadeBlock = 128;
-constexpr int kShadeBpcW3 = 24;       // k_shade_w3 blocks per CU (four rounds of its 6 resident blocks)
+constexpr int kShadeBpcW3 = 36;       // k_shade_w3 blocks per CU (six rounds of its 6 resident blocks; 24: C2 k_shade 5.97 vs 5.88 ms)
 constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h
 constexpr int kLdsSceneMax = 16384;  // bytes of BVH nodes + prim records staged in LDS by k_trace<true>
 constexpr size_t kTabLdsMax = 8192;   // bytes of scene tables k_shade_tab stages in LDS after the Halton tables
