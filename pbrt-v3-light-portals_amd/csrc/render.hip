@@ -275,7 +275,7 @@ struct pt_scene {
     bool cb_spill = false;
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
-    int shade_bpc = 8;           // shading blocks per CU (grid-stride; PT_SHADE_BPC)
+    int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
