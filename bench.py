@@ -32,6 +32,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "Msamples/sec + Mrays/sec, 1920x1080 path integrator @256spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+LDS_PEAK_GBS = 256 * 128 * 2.4  # 256 CUs x 128 B/clk x 2.4 GHz: the roof of an LDS-resident scene's node / prim reads
 # BASELINE.json configs this bench can run: scene file, workload label
 CONFIGS = {
     "c2": ("portal_cornell.pbrt", "portal Cornell (config 2)", "path maxdepth 5",
@@ -197,7 +198,10 @@ def rooflines(agg: dict, workload: str, lds_scene: bool) -> dict:
             "WRITE_SIZE passes)", "traffic_source": k["traffic_source"], "kernel": dom,
             "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"]}
     if on_chip:
-        roof["note"] = "dominant kernel reads its scene from LDS: achieved = measured HBM bytes / launch time"
+        roof["note"] = ("dominant kernel reads its scene from LDS: achieved = measured HBM bytes / launch time; "
+                        "lds_view sets its SURVEY 8(d) bytes (LDS reads) against the LDS roof")
+        roof["lds_view"] = {"achieved": k["algorithmic_GBs"], "peak": round(LDS_PEAK_GBS, 1), "unit": "GB/s",
+                            "frac": round(k["algorithmic_GBs"] / LDS_PEAK_GBS, 5)}
     return {"roofline": roof, "roofline_kernels": ks}
 
 
