@@ -32,7 +32,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "Msamples/sec + Mrays/sec, 1920x1080 path integrator @256spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-LDS_PEAK_GBS = 256 * 128 * 2.4  # 256 CUs x 128 B/clk x 2.4 GHz: the roof of an LDS-resident scene's node / prim reads
+LDS_B128_PEAK_GBS = 150000.0  # ds_read_b64/b128 aggregate, every CU streaming (MI355X_MICROARCH.md LDS section)
 # BASELINE.json configs this bench can run: scene file, workload label
 CONFIGS = {
     "c2": ("portal_cornell.pbrt", "portal Cornell (config 2)", "path maxdepth 5",
@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--shard", default="tiles", help="tiles (strong, default) | samples-split (strong) | samples (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-parity", action="store_true", help="skip the GPU-vs-oracle film check of the cpu_baseline tiles")
+    ap.add_argument("--emulate-ranks", default="",
+                    help="comma-separated rank counts (e.g. 2,4,8): time every rank's tile shard on this GPU, one "
+                         "after the other, and predict the strong-scaling efficiency (single process only)")
+    ap.add_argument("--print-source-hash", action="store_true", help="print source_hash() and exit")
     return ap.parse_args()
 
 
@@ -93,7 +98,7 @@ REFERENCE_PROBE = {"value": 0.684, "unit": "Msamples/s", "cores": 8,
                              "draft C2 scene at 480x270 @16 spp scaled to the frame (not re-run here)"}
 
 
-def cpu_baseline(scene_path: str, seconds: float) -> dict:
+def cpu_baseline(scene_path: str, seconds: float):
     """Reference CPU path restated in C (oracle/, 'port'), timed on this host's
     cores on a bounded sample of the same frame: the 16x16 tiles t with
     t % stride == 0, spread over the whole image (stride sized so the timed
@@ -118,7 +123,7 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
     want = max(2 * threads, min(ntiles, st["samples"] / dt * seconds / per_tile))
     stride = max(1, int(ntiles // want))
     t0 = time.perf_counter()
-    _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
+    film, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
     rate = st["samples"] / dt / 1e6
     host = os.cpu_count() or threads
@@ -132,62 +137,129 @@ def cpu_baseline(scene_path: str, seconds: float) -> dict:
                       f"at the scene's spp ({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
             "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3),
             "per_thread": round(rate / threads, 4),
-            "reference_probe": dict(REFERENCE_PROBE, per_thread=round(REFERENCE_PROBE["value"] / 8, 4))}
+            "reference_probe": dict(REFERENCE_PROBE, per_thread=round(REFERENCE_PROBE["value"] / 8, 4))}, \
+        (stride, film, st)
 
 
-def pmc_traffic(workload: str, kernel: str = "k_trace"):
-    """HBM bytes per launch of the traversal kernel (name containing `kernel`;
-    the variant with the most launches) from the newest committed PMC summary
-    (profiles/r*_pmc_traffic.json, made by scripts/pmc_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench on
-    the same workload), or (None, None) when there is none."""
+def source_hash() -> str:
+    """Hash of the sources libptgpu.so is built from (csrc/, include/pt.h, the
+    Makefile): a profile summary records the hash of the tree it was taken on,
+    and the bench uses its counters only when they match (no git on the GPU
+    box, so no commit lookup)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG, "csrc")
+    files = [os.path.join(csrc, f) for f in sorted(os.listdir(csrc))]
+    files += [os.path.join(REPO, "include", "pt.h"), os.path.join(PKG, "Makefile")]
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _profile_files(pattern: str):
     import glob
     import re
-    files = glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json"))
-    files.sort(key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
-    for f in reversed(files):
+    files = glob.glob(os.path.join(REPO, "profiles", pattern))
+    files.sort(key=lambda f: (int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)), os.path.getmtime(f)))
+    return list(reversed(files))
+
+
+def _kernel_match(name: str, kernel: str) -> bool:
+    """rocprof kernel names look like 'void pt::k_shade_w3<16>': match the
+    exact kernel (k_shade must not match k_shade_w3)."""
+    base = name.replace("void ", "").split("<")[0].split("::")[-1]
+    return base == kernel
+
+
+def pmc_traffic(workload: str, kernel: str, src: str):
+    """HBM bytes per launch of `kernel` (the variant with the most launches)
+    from the newest committed PMC summary (profiles/r*_pmc_traffic.json, made
+    by scripts/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench on the same workload) taken on the same
+    sources (source_hash).  Returns (bytes, file, stale_file): a summary of
+    other sources is never used, only named in stale_file."""
+    stale = None
+    for f in _profile_files("r*_pmc_traffic.json"):
         d = json.load(open(f))
         if d.get("workload") != workload:
             continue
-        ks = [(v["launches"], v["hbm_bytes_per_launch"]) for k, v in d.get("kernels", {}).items() if kernel in k]
-        if ks:
-            return max(ks)[1], os.path.relpath(f, REPO)
-    return None, None
+        ks = [(v["launches"], v["hbm_bytes_per_launch"]) for k, v in d.get("kernels", {}).items()
+              if _kernel_match(k, kernel)]
+        if not ks:
+            continue
+        if d.get("source_hash") != src:
+            stale = stale or os.path.relpath(f, REPO)
+            continue
+        return max(ks)[1], os.path.relpath(f, REPO), None
+    return None, None, stale
 
 
-def rooflines(agg: dict, workload: str, lds_scene: bool) -> dict:
-    """roofline = the dominant kernel by measured time (HIP events around every
-    launch on its stream); both kernels' figures under roofline_kernels.
+def sq_issue_view(config: str, kernel: str, src: str):
+    """Issue / wait shares of `kernel` from the newest SQ-counter summary of
+    this config taken on the same sources (profiles/r*_sq_counters.json,
+    scripts/sq_summary.py), or None."""
+    for f in _profile_files("r*_sq_counters.json"):
+        d = json.load(open(f))
+        if d.get("source_hash") != src or d.get("config") != config:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if _kernel_match(k, kernel):
+                keys = ("active_inst_any_share", "wait_any_share", "wait_inst_any_share", "insts_per_wave_valu",
+                        "insts_per_wave_salu", "insts_per_wave_lds")
+                return dict({x: round(v[x], 4) for x in keys if x in v}, source=os.path.relpath(f, REPO),
+                            bench_args=d.get("bench_args"))
+    return None
 
-    * k_trace: algorithmic bytes per SURVEY §8(d), 32 B per node visit + 48 B
-      per primitive test, counted on the device.  For a scene whose BVH fits
-      LDS (C2) those bytes are LDS reads, not HBM traffic: the kernel is then
-      labelled on-chip / latency-bound and only its PMC-measured HBM bytes
-      (rays in, hits out) are set against the HBM peak.
-    * k_shade: the path-state bytes each path step must read and write (the
-      SoA fields PathIntegrator::Li carries between vertices + queue
-      entries), counted on the device per step (kernels.hip shade_path)."""
+
+def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: bool, names: tuple, src: str) -> dict:
+    """roofline = the kernel that dominates the TIMED region (HIP events on
+    its stream around every launch of the K timed steps, two pipelines
+    overlapping); both kernels' figures under roofline_kernels, with their
+    per-launch times in the timed region (what rocprofv3 --stats averages)
+    and in one isolated frame (batches one after the other).
+
+    * traversal: algorithmic bytes per SURVEY 8(d), 32 B per LinearBVHNode
+      visit (bvh.cpp:95-104) + 48 B per primitive test (triangle.cpp:189-425),
+      counted on the device.  For a scene whose BVH sits in LDS (C2-C4) those
+      are LDS reads: set against the ds_read_b128 aggregate (MI355X_MICROARCH
+      LDS table, ~150 TB/s), with the SQ issue view beside it.
+    * shading: the path-state bytes each path step must read and write (the
+      state PathIntegrator::Li carries between vertices + queue entries),
+      counted on the device per step (kernels.hip shade_path)."""
+    trace_name, shade_name = names
     ks = {}
-    tl, sl = max(1, agg["trace_launches"]), max(1, agg["shade_launches"])
-    alg_t = (32.0 * agg["node_visits"] + 48.0 * agg["prim_tests"]) / tl
-    avg_t = agg["trace_ms"] / tl
-    trf_t, src_t = pmc_traffic(workload, "k_trace")
-    ks["k_trace"] = {"avg_launch_ms": round(avg_t, 4), "algorithmic_bytes_per_launch": round(alg_t, 1),
-                     "algorithmic_GBs": round(alg_t / (avg_t * 1e-3) / 1e9, 1) if avg_t > 0 else 0.0,
-                     "data": "LDS (BVH + primitives staged per block): on-chip, latency-bound" if lds_scene else "HBM",
-                     "hbm_traffic_per_launch": round(trf_t, 1) if trf_t is not None else None,
-                     "hbm_GBs": round(trf_t / (avg_t * 1e-3) / 1e9, 1) if (trf_t is not None and avg_t > 0) else None,
-                     "traffic_source": src_t, "total_ms": round(agg["trace_ms"], 2)}
-    if agg["shade_bytes"] > 0:
-        alg_s = agg["shade_bytes"] / sl
-        avg_s = agg["shade_ms"] / sl
-        trf_s, src_s = pmc_traffic(workload, "k_shade")
-        ks["k_shade"] = {"avg_launch_ms": round(avg_s, 4), "algorithmic_bytes_per_launch": round(alg_s, 1),
-                         "algorithmic_GBs": round(alg_s / (avg_s * 1e-3) / 1e9, 1) if avg_s > 0 else 0.0,
-                         "data": "HBM (path state)",
-                         "hbm_traffic_per_launch": round(trf_s, 1) if trf_s is not None else None,
-                         "hbm_GBs": round(trf_s / (avg_s * 1e-3) / 1e9, 1) if (trf_s is not None and avg_s > 0) else None,
-                         "traffic_source": src_s, "total_ms": round(agg["shade_ms"], 2)}
+    parts = [("k_trace", trace_name, "trace", 32.0 * timed["node_visits"] + 48.0 * timed["prim_tests"])]
+    if timed["shade_bytes"] > 0:
+        parts.append(("k_shade", shade_name, "shade", float(timed["shade_bytes"])))
+    for key, kname, p, alg_total in parts:
+        nl = max(1, timed[p + "_launches"])
+        avg = timed[p + "_ms"] / nl
+        alg = alg_total / nl
+        il = max(1, iso[p + "_launches"])
+        trf, trf_src, stale = pmc_traffic(workload, kname, src)
+        e = {"kernel": kname, "launches": timed[p + "_launches"], "avg_launch_ms": round(avg, 4),
+             "isolated_avg_launch_ms": round(iso[p + "_ms"] / il, 4),
+             "algorithmic_bytes_per_launch": round(alg, 1),
+             "algorithmic_GBs": round(alg / (avg * 1e-3) / 1e9, 1) if avg > 0 else 0.0,
+             "data": ("LDS (BVH + primitives staged per block)" if (p == "trace" and lds_scene) else
+                      ("HBM (path state)" if p == "shade" else "HBM")),
+             "hbm_traffic_per_launch": round(trf, 1) if trf is not None else None,
+             "hbm_GBs": round(trf / (avg * 1e-3) / 1e9, 1) if (trf is not None and avg > 0) else None,
+             "traffic_source": trf_src, "total_ms": round(timed[p + "_ms"], 2)}
+        if trf is not None:
+            e["traffic_over_algorithmic"] = round(trf / alg, 3) if alg > 0 else None
+        if stale:
+            e["traffic_stale"] = stale + " (taken on other sources: not used)"
+        if p == "trace" and lds_scene:
+            e["lds_view"] = {"achieved": e["algorithmic_GBs"], "peak": LDS_B128_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(e["algorithmic_GBs"] / LDS_B128_PEAK_GBS, 5),
+                             "note": "SURVEY 8(d) bytes read from LDS vs the ds_read_b128 aggregate"}
+            iv = sq_issue_view(config, kname, src)
+            if iv:
+                e["issue_view"] = iv
+        ks[key] = e
     dom = max(ks, key=lambda k: ks[k]["total_ms"])
     k = ks[dom]
     on_chip = dom == "k_trace" and lds_scene
@@ -195,18 +267,62 @@ def rooflines(agg: dict, workload: str, lds_scene: bool) -> dict:
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved is not None else None,
             "traffic": k["hbm_traffic_per_launch"], "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + "
-            "WRITE_SIZE passes)", "traffic_source": k["traffic_source"], "kernel": dom,
-            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"]}
+            "WRITE_SIZE passes on the same sources)", "traffic_source": k["traffic_source"], "kernel": k["kernel"],
+            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"],
+            "dominant_by": "kernel time in the timed steps",
+            "recipe": "achieved = algorithmic_bytes_per_launch / avg_launch_ms (HIP events, timed region); "
+                      "frac = achieved / peak"}
     if on_chip:
         roof["note"] = ("dominant kernel reads its scene from LDS: achieved = measured HBM bytes / launch time; "
-                        "lds_view sets its SURVEY 8(d) bytes (LDS reads) against the LDS roof")
-        roof["lds_view"] = {"achieved": k["algorithmic_GBs"], "peak": round(LDS_PEAK_GBS, 1), "unit": "GB/s",
-                            "frac": round(k["algorithmic_GBs"] / LDS_PEAK_GBS, 5)}
+                        "its LDS view is under roofline_kernels.k_trace.lds_view")
+        roof["recipe"] = "achieved = PMC HBM bytes per launch / avg_launch_ms; frac = achieved / peak"
     return {"roofline": roof, "roofline_kernels": ks}
+
+
+def parity_check(sc, hs, stride: int, ref_acc, ref_st: dict) -> dict:
+    """The GPU film of the tiles t % stride == 0 (the cpu_baseline's sample of
+    the same frame), rendered with the production batch size and pipelines,
+    against the oracle's film of the same tiles: bit-exact pixels of the film
+    (XYZ + weight, Film::Pixel), RMSE of the resolved image, and the
+    reference's ray / node / primitive counters (integrator.cpp:526-637)."""
+    import numpy as np
+    got, gst = sc.render_accum(0, stride)
+    same = np.all(got.view(np.uint32) == ref_acc.view(np.uint32), axis=2)
+    touched = np.any(ref_acc != 0, axis=2) | np.any(got != 0, axis=2)
+    a = sc.resolve(got).astype(np.float64)
+    b = sc.resolve(ref_acc).astype(np.float64)
+    rmse = float(np.sqrt(np.mean((a - b) ** 2)))
+    keys = ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests")
+    return {"tiles": f"t % {stride} == 0", "samples": int(gst["samples"]),
+            "bit_exact_pixels": round(float(np.mean(same)), 6),
+            "bit_exact_rendered_pixels": round(float(np.mean(same[touched])), 6) if touched.any() else None,
+            "rendered_pixels": int(touched.sum()), "rmse": rmse,
+            "counters_equal": all(int(gst[k]) == int(ref_st[k]) for k in keys),
+            "batch_slots": int(sc.query("batch_slots")) or None, "pipelines": int(sc.query("pipelines")),
+            "oracle": "oracle/pt_oracle.c render_accum of the same tiles"}
+
+
+def emulated_scaling(rank_ms: dict, frame_ms: float, frame_samples: float) -> dict:
+    """Strong-scaling prediction on one GPU (--emulate-ranks): rank_ms[N] is
+    the device time of every rank's shard (tiles t % N == r) rendered one
+    after the other; a step at N ranks takes the slowest shard (plus the
+    film reduce, not included).  efficiency = (frame_ms / N) / max shard."""
+    out = {}
+    for n, times in sorted(rank_ms.items()):
+        mx = max(times)
+        out[str(n)] = {"per_rank_ms": [round(t, 2) for t in times], "max_ms": round(mx, 2),
+                       "mean_ms": round(sum(times) / len(times), 2),
+                       "imbalance": round(mx / (sum(times) / len(times)), 4),
+                       "predicted_msamples_per_s": round(frame_samples / (mx * 1e-3) / 1e6, 2),
+                       "predicted_efficiency": round(frame_ms / n / mx, 4)}
+    return {"frame_ms_1gpu": round(frame_ms, 2), "excludes": "the per-step ncclReduce of the film", "ranks": out}
 
 
 def main():
     args = parse()
+    if args.print_source_hash:
+        print(source_hash())
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -226,6 +342,7 @@ def main():
     sc = ptgpu.Scene(hs, device=local, batch_slots=args.batch_slots or None)
     w, h = sc.film_size()
     lds_scene = sc.query("trace_lds_bytes") > 0  # the library stages this BVH in LDS (PT_TRACE_LDS honoured)
+    names = sc.kernel_names()
     import re
     spp = int(re.search(r'"integer pixelsamples" \[(\d+)\]', open(spath).read()).group(1))
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -277,10 +394,10 @@ def main():
     rank_times = shardmod.gather_rank_times(agg["render_ms"] / args.steps, agg["reduce_ms"] / args.steps, world,
                                             device=f"cuda:{local}")
 
-    # Kernel rooflines from one more frame with the batches run one after the
-    # other (pt_set_pipelines(1)): in the timed region two pipelines overlap
-    # one batch's trace with another's shading, so per-launch times there
-    # include the co-running kernel.  This rank's shard, no collective.
+    # One more frame with the batches run one after the other
+    # (pt_set_pipelines(1)): per-launch times of each kernel alone, reported
+    # beside the timed region's (where two pipelines overlap one batch's trace
+    # with another's shading).  This rank's shard, no collective.
     iso = {"trace_ms": 0.0, "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0,
            "node_visits": 0, "prim_tests": 0}
     pipes = sc.query("pipelines")
@@ -291,8 +408,20 @@ def main():
     sc.set_pipelines(pipes)
     for k in iso:
         iso[k] = st[k]
-    overlapped = {"k_trace_avg_launch_ms": round(agg["trace_ms"] / max(1, agg["trace_launches"]), 4),
-                  "k_shade_avg_launch_ms": round(agg["shade_ms"] / max(1, agg["shade_launches"]), 4)}
+    emul = None
+    if args.emulate_ranks and world == 1:
+        # every rank's tile shard at N ranks, one after the other, each timed like a step
+        rank_ms = {}
+        for n in sorted({int(v) for v in args.emulate_ranks.split(",") if v.strip()}):
+            rank_ms[n] = []
+            for r_ in range(n):
+                accum.zero_()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                render(shardmod.plan(r_, n, spp, "tiles"))
+                torch.cuda.synchronize()
+                rank_ms[n].append((time.perf_counter() - t0) * 1e3)
+        emul = emulated_scaling(rank_ms, dt / args.steps * 1e3, total_samples / args.steps)
 
     if rank == 0:
         cname, cdepth, cdata = CONFIGS[args.config][1:]
@@ -318,12 +447,15 @@ def main():
             "rays_per_sample": round(total_rays / max(1.0, total_samples), 3),
             "rank_times": rank_times,
         }
-        out.update(rooflines(iso, workload, lds_scene))
-        out["roofline"]["timing"] = ("kernel launches timed with HIP events in one frame with the batches "
-                                     "run one after the other; the timed steps overlap two batches "
-                                     "(per-launch times there: %s)" % json.dumps(overlapped))
+        src = source_hash()
+        out["source_hash"] = src
+        out.update(rooflines(agg, iso, workload, args.config, lds_scene, names, src))
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(spath, args.cpu_seconds)
+            out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds)
+            if not args.no_parity:
+                out["parity"] = parity_check(sc, hs, stride, ref_acc, ref_st)
+        if emul is not None:
+            out["emulated_scaling"] = emul
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 9
+#define PT_ABI_VERSION 10
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -361,7 +361,9 @@ pt_status pt_render_range(pt_scene* scene, int tile_offset, int tile_stride,
  * (any launcher channel); each rank selects its GPU (pt_init(1, &id)) and calls
  * pt_comm_create.  pt_render_frame_dist renders the tiles t % nranks == rank
  * into d_accum (zeroed by the call) on `stream` and sums the films onto rank 0
- * with one ncclReduce -- the frame's only collective. */
+ * with one ncclReduce -- the frame's only collective.  It returns after that
+ * reduce has completed on `stream` (the host waits for it: stats->reduce_ms is
+ * read back from events around it). */
 #define PT_COMM_ID_BYTES 128
 typedef struct pt_comm pt_comm;
 pt_status pt_comm_unique_id(uint8_t* id_out);
@@ -412,7 +414,10 @@ enum pt_scene_key {
     PT_Q_BATCH_SLOTS = 1,      /* pt_set_batch_slots value (0 = the default) */
     PT_Q_TRACE_LDS_BYTES = 2,  /* bytes of BVH + primitives the trace kernel stages in LDS (0 = reads HBM) */
     PT_Q_TRACE_SPILL = 3,      /* 1 when traversal stacks spill past the LDS rows (deep BVHs) */
-    PT_Q_FEATURES = 4          /* scene-feature set the shading kernel is instantiated for */
+    PT_Q_FEATURES = 4,         /* scene-feature set the shading kernel is instantiated for */
+    PT_Q_TRACE_KERNEL = 5,     /* traversal kernel of a render: 0 k_trace, 1 k_trace_pt, 2 k_trace_nb, 3 k_trace_lds */
+    PT_Q_SHADE_KERNEL = 6      /* shading kernel: 0 k_shade, 3 k_shade_w3, 5 k_shade_tab, 6 k_shade_dl,
+                                  7 / 8 / 9 k_shade_hero / _w2 / _w4 */
 };
 pt_status pt_scene_query(const pt_scene* scene, int32_t key, int64_t* value);
 

@@ -107,6 +107,10 @@ int oracle_camera_ray(const pt_scene_desc* desc, float film_x, float film_y,
 int oracle_test_reintersect(int i, int n_dirs, float* tri9, float* rays7, int* self_hits);
 int oracle_test_triangle_sampling(int i, int count, double* unif, double* tri_est, float* tri9, float* pc3,
                                   int* bad_pdf);
+/* FullSphere.Reintersect / PartialSphere.Normal / PartialSphere.Reintersect
+ * (src/tests/shapes.cpp:428-498) for RNG seed i (see pt_oracle.c). */
+int oracle_test_sphere(int i, int partial, int mode, int n_dirs, float* params4, float* rays7, int* self_hits,
+                       float* out);
 int oracle_triangle_intersect(const float tri9[9], const float ray7[7], int any, float* t);
 int oracle_dist1d(const float* func, int n, int mode, float u, float* out);
 

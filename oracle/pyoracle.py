@@ -72,6 +72,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_test_triangle_sampling.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                     ctypes.POINTER(ctypes.c_double), vp, vp,
                                                     ctypes.POINTER(ctypes.c_int)]
+        L.oracle_test_sphere.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
+                                         ctypes.POINTER(ctypes.c_int), vp]
         L.oracle_triangle_intersect.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         L.oracle_dist1d.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_float, vp]
         _lib = L
@@ -224,6 +226,25 @@ def triangle_sampling_case(i: int, count: int = 512 * 1024):
     ok = lib().oracle_test_triangle_sampling(i, count, ctypes.byref(a), ctypes.byref(b), tri.ctypes.data,
                                              pc.ctypes.data, ctypes.byref(bad))
     return (a.value, b.value, tri.reshape(3, 3), pc, bad.value) if ok else None
+
+
+def sphere_case(i: int, partial: bool, mode: str, n_dirs: int = 10000):
+    """The Sphere cases of src/tests/shapes.cpp (FullSphere.Reintersect,
+    PartialSphere.Normal / Reintersect) for RNG seed i, or None when the
+    reference skips the seed (its first ray misses).  mode 'reintersect' ->
+    (params (radius, zmin, zmax, phimax), spawned rays (2*n_dirs, 7),
+    self-hit count); mode 'normal' -> (params, dot(n, p) normalised)."""
+    params = np.zeros(4, np.float32)
+    out = np.zeros(1, np.float32)
+    bad = ctypes.c_int()
+    if mode == "reintersect":
+        rays = np.zeros((2 * n_dirs, 7), np.float32)
+        ok = lib().oracle_test_sphere(i, int(partial), 0, n_dirs, params.ctypes.data, rays.ctypes.data,
+                                      ctypes.byref(bad), out.ctypes.data)
+        return (params, rays, bad.value) if ok else None
+    ok = lib().oracle_test_sphere(i, int(partial), 1, 0, params.ctypes.data, None, ctypes.byref(bad),
+                                  out.ctypes.data)
+    return (params, float(out[0])) if ok else None
 
 
 def triangle_intersect(tri9, ray7, any_hit: bool = False):

@@ -98,9 +98,6 @@ struct DevScene {
     const float4* prims;
     int n_nodes;
     int n_prims;
-    // child-pair records (k_trace_cb): 4 x float4 per interior node, both children's boxes + references
-    const float4* crec;
-    int cb_root;  // the root's reference (node 0 or its leaf encoding)
     const pt_triangle* tris;
     const float* P;
     const float* N;

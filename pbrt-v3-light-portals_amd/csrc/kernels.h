@@ -20,8 +20,7 @@ constexpr uint32_t kTraceChunk = 512;  // ray-queue entries a k_trace_nb wave ta
 constexpr int kNodeSteps = PT_NODE_STEPS;
 constexpr int kLeafSteps = PT_LEAF_STEPS;
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
-constexpr int kCbSpillWords = 128;  // k_trace_cb: global spill per lane, two words per entry
-constexpr int kCbStackRows = kStackLds;  // k_trace_cb LDS stack rows (x2 words: 20 KB per block, 4 waves per SIMD)
+constexpr int kSpillWords = 64 - kStackLds;  // k_trace_pt: global spill entries per lane beyond the LDS rows
 constexpr int kShadeBlock = 128;
 constexpr int kShadeBpcW3 = 36;       // k_shade_w3 blocks per CU (six rounds of its 6 resident blocks; 24: C2 k_shade 5.97 vs 5.88 ms)
 constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h

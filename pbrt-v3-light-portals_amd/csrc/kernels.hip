@@ -509,225 +509,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
 #endif
 
 // ----------------------------------------------------------------------------
-// k_trace_cb: k_trace_pt over child-pair records (HBM-resident BVHs).
-//
-// BVHAccel::Intersect visits a node by testing its box; an interior node then
-// pushes its far child and the near child's box is tested next.  Of
-// Bounds3::IntersectP's result only the final `tMin < ray.tMax` depends on the
-// ray's current tMax, so a box's part of the test that does not (the slab
-// overlaps and tMax > 0) and its entry distance can be computed whenever the
-// box is at hand.  Here the record of interior node X (sc.crec, 64 B, indexed
-// like the binary node) holds both children's boxes and references: one load
-// tests both children; the near child is visited next (its `entry < tMax`
-// with the same tMax the reference would use: no primitive is tested in
-// between), the far child is pushed with its entry distance (NaN when the
-// tMax-independent part failed) and tested against the tMax current when it
-// is popped -- the reference's test, at the reference's time.  Node visits,
-// primitive tests, their order and every tMax update are the reference's, so
-// hits and counters are identical; what changes is that a node is loaded only
-// when its box passed and it is interior (a culled node, pushed or near,
-// costs no load, and a leaf's box comes with its parent).  Child reference:
-// interior = node index; leaf = 0x80000000 | count << 24 | first primitive
-// (create_scene_on builds records only when every leaf fits that encoding).
-// ----------------------------------------------------------------------------
-// node_box_hit without its tMax comparison: the entry distance when the
-// tMax-independent part passes, else NaN (node_box_hit == entry < ray.tmax)
-__device__ __forceinline__ float box_entry(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2) {
-    const float kx = 1 + 2 * gammaf(3);
-    float tMin = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
-    float tMax = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
-    const float tyMin = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
-    float tyMax = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
-    const float tzMin = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
-    float tzMax = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
-    tMax *= kx;
-    tyMax *= kx;
-    tzMax *= kx;
-    const bool ok1 = !(tMin > tyMax) & !(tyMin > tMax);
-    tMin = tyMin > tMin ? tyMin : tMin;
-    tMax = tyMax < tMax ? tyMax : tMax;
-    const bool ok2 = !(tMin > tzMax) & !(tzMin > tMax);
-    tMin = tzMin > tMin ? tzMin : tMin;
-    tMax = tzMax < tMax ? tzMax : tMax;
-    return (ok1 & ok2 & (tMax > 0)) ? tMin : __int_as_float(0x7fc00000);
-}
-// PT_TRACE_CB_WAVES (experiment builds): force the waves-per-SIMD register budget
-#ifdef PT_TRACE_CB_WAVES
-#define PT_TRACE_CB_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_CB_WAVES)))
-#else
-#define PT_TRACE_CB_ATTR
-#endif
-template <bool kSpill, bool kSph>
-__global__ __launch_bounds__(kTraceBlock) PT_TRACE_CB_ATTR void k_trace_cb(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
-                                                          const uint32_t* __restrict__ rq_count, uint32_t* fetch,
-                                                          int refill_min, int leaf_min, int stack_rows, int* spill,
-                                                          DevStats* stats)
-#ifdef PT_TU_TRACE
-{
-    // LDS stack: stack_rows rows of child references, then as many of entry
-    // distances; deeper entries go to the lane's global spill (two words each)
-    extern __shared__ float4 lds_dyn[];
-    int* stk = (int*)lds_dyn;
-    float* stt = (float*)(stk + stack_rows * kTraceBlock);
-    const float4* __restrict__ rec = sc.crec;
-    const float4* __restrict__ bprims = sc.prims;
-    const uint32_t n = *rq_count;
-    const int tid = threadIdx.x;
-    const uint32_t lane = lane_id();
-    int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * kCbSpillWords;
-    uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
-    bool active = false, exhausted = false, drained = false;
-    uint32_t qn = 0, qe = 0;
-    uint32_t slot = 0, kind = 0;
-    Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
-    V3 inv = v3(0, 0, 0);
-    TriShear sh{0, 0, 0, 0};
-    bool n0 = false, n1 = false, n2 = false;
-    int pend = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
-    float pendT = 0.f;  // the pending node's entry distance (NaN: its box test fails whatever tMax)
-    auto pop = [&]() {
-        --toVisit;
-        if (!kSpill || toVisit < stack_rows) {
-            pend = stk[toVisit * kTraceBlock + tid];
-            pendT = stt[toVisit * kTraceBlock + tid];
-        } else {
-            pend = myspill[2 * (toVisit - stack_rows)];
-            pendT = __int_as_float(myspill[2 * (toVisit - stack_rows) + 1]);
-        }
-    };
-    for (;;) {
-        if (!exhausted) {
-            const uint64_t idle = __ballot(!active);
-            const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle > 0 && (nidle >= (uint32_t)refill_min || nidle == 64u)) {
-                if (qn >= qe && !drained) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
-                    qn = base < n ? base : n;
-                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
-                    drained = base + kTraceChunk >= n;
-                }
-                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
-                const uint32_t k = lanes_below(idle);
-                const uint32_t i = qn + k;
-                qn += take;
-                if (drained && qn >= qe) exhausted = true;
-                if (!active) {
-                    if (k < take) {
-                        const uint32_t e = rq[i];
-                        slot = e >> 2;
-                        kind = e & 3u;
-                        ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
-                        inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
-                        sh = tri_shear(ray.d);
-                        n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
-                        toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
-                        active = sc.n_nodes > 0;  // empty scene: every ray misses
-                        if (active) {  // the root's box (its visit is the first node step)
-                            pend = sc.cb_root;
-                            pendT = box_entry(sc.nodes[0], sc.nodes[1], ray, inv, n0, n1, n2);
-                        } else {
-                            if (kind == kRayShadow) ps.hitA[slot] = 0;
-                            else if (kind == kRayCont) ps.hit[slot] = -1;
-                            else if (kind == kRayA) ps.hitA[slot] = -1;
-                            else ps.hitB[slot] = -1;
-                        }
-                        if (kind == kRayShadow) ++nsh; else ++ncl;
-                    }
-                }
-            }
-        }
-        if (__ballot(active) == 0) {
-            if (exhausted) break;
-            continue;
-        }
-        const bool wantLeaf = active && leafPos < leafEnd;
-        const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wantLeaf));
-        const uint32_t nNode = (uint32_t)__popcll(__ballot(active && !wantLeaf));
-        const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
-        ++iters;
-        if (!active || wantLeaf != leafStep) continue;
-        bool done = false;
-        if (leafStep) {
-#pragma unroll
-            for (int u = 0; u < kLeafSteps; ++u) {
-                if (u > 0 && (done || leafPos >= leafEnd)) continue;
-                const int pi = leafPos++;
-                ++prims;
-                const float4 r0 = bprims[3 * pi];
-                const float4 r1 = bprims[3 * pi + 1];
-                const uint32_t fl = __float_as_uint(r0.w);
-                float t;
-                bool ok;
-                if (fl & kPrimAnalytic) {
-                    ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
-                } else {
-                    const float4 r2 = bprims[3 * pi + 2];
-                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
-                    if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
-                }
-                if (ok) {
-                    hitPrim = pi;
-                    if (kind == kRayShadow) done = true;
-                    else ray.tmax = t;
-                }
-                if (!done && leafPos == leafEnd) {
-                    if (toVisit == 0) done = true;
-                    else pop();
-                }
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kNodeSteps; ++u) {  // up to kNodeSteps node visits while in node mode
-                if (u > 0 && (done || leafPos < leafEnd)) continue;
-                ++nodes;  // the visit of the pending node: its box test
-                if (!(pendT < ray.tmax)) {
-                    if (toVisit == 0) done = true;
-                    else pop();
-                } else if (pend < 0) {  // a leaf: its primitives next
-                    leafPos = pend & 0xffffff;
-                    leafEnd = leafPos + ((pend >> 24) & 0x7f);
-                } else {
-                    const float4 r0 = rec[4 * pend], r1 = rec[4 * pend + 1];
-                    const float4 r2 = rec[4 * pend + 2], r3 = rec[4 * pend + 3];
-                    const float tA = box_entry(r0, r1, ray, inv, n0, n1, n2);  // first child (the node after X)
-                    const float tB = box_entry(r2, r3, ray, inv, n0, n1, n2);  // second child
-                    const int refA = __float_as_int(r1.z), refB = __float_as_int(r1.w);
-                    const int axis = __float_as_int(r3.z);
-                    const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
-                    const int far = neg ? refA : refB;
-                    const float farT = neg ? tA : tB;
-                    if (!kSpill || toVisit < stack_rows) {
-                        stk[toVisit * kTraceBlock + tid] = far;
-                        stt[toVisit * kTraceBlock + tid] = farT;
-                    } else {
-                        myspill[2 * (toVisit - stack_rows)] = far;
-                        myspill[2 * (toVisit - stack_rows) + 1] = __float_as_int(farT);
-                    }
-                    ++toVisit;
-                    pend = neg ? refB : refA;
-                    pendT = neg ? tB : tA;
-                }
-            }
-        }
-        if (done) {
-            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
-            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
-            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
-            else ps.hitB[slot] = hitPrim;
-            active = false;
-        }
-    }
-    flush_stats(stats, ncl, nsh, nodes, prims);
-    const unsigned long long itw = wave_sum_u64(iters);
-    if (lane == 0 && itw) atomicAdd(&stats->lane_iters, itw);
-}
-#else
-;
-#endif
-
-// ----------------------------------------------------------------------------
 // k_trace_nb: k_trace_pt with the per-step control flow replaced by selects
 // (the traversal is the same; only which instructions run changes).  The
 // stack push is an unconditional LDS store above the top; the pop an

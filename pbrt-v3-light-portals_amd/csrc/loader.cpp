@@ -914,22 +914,46 @@ class Loader {
             std::vector<float> P, N, S, UV;
             std::vector<int> idx;
             if (name == "trianglemesh") {
+                // CreateTriangleMeshShape (triangle.cpp:911-971): missing indices or P, or an index past the
+                // last vertex, is an Error() that yields no shapes (and so no area lights) while the scene
+                // goes on; a uv / S / N array of the wrong length is discarded.  Empty arrays ("point P" [])
+                // are present with zero values: a mesh of zero triangles.  Counts follow the parser
+                // (parser.cpp:523-615): a point / normal / vector array keeps its whole triples, a uv array
+                // its whole pairs, and only nvi / 3 triangles are made.
                 const Param* pi = ps.find("indices", {"integer"});
                 const Param* pp = ps.find("P", {"point"});
-                if (!pp || pp->nums.size() % 3 != 0 || pp->nums.empty())
-                    throw PtError(PT_ERR_PARSE, "trianglemesh needs \"point P\"");
-                const int nv = (int)pp->nums.size() / 3;
-                if (pi) for (double v : pi->nums) idx.push_back(int(v));
-                else if (nv == 3) idx = {0, 1, 2};
-                else throw PtError(PT_ERR_PARSE, "trianglemesh needs \"integer indices\"");
-                const Param* pn = ps.find("N", {"normal"});
-                const Param* pS = ps.find("S", {"vector"});
                 const Param* puv = ps.find("uv", {"point2", "float"});
                 if (!puv) puv = ps.find("st", {"point2", "float"});
-                for (double v : pp->nums) P.push_back((float)v);
-                if (pn && (int)pn->nums.size() == 3 * nv) for (double v : pn->nums) N.push_back((float)v);
-                if (pS && (int)pS->nums.size() == 3 * nv) for (double v : pS->nums) S.push_back((float)v);
-                if (puv && (int)puv->nums.size() == 2 * nv) for (double v : puv->nums) UV.push_back((float)v);
+                const int nv = pp ? (int)(pp->nums.size() / 3) : 0;
+                const int nuv = puv ? (int)(puv->nums.size() / 2) : 0;
+                bool useUV = puv != nullptr && nuv > 0;
+                if (useUV && nuv < nv) {
+                    warn("Not enough of \"uv\"s for triangle mesh.  Expected " + std::to_string(nv) + ", found " +
+                         std::to_string(nuv) + ".  Discarding.");
+                    useUV = false;
+                }
+                if (!pi) { warn("Vertex indices \"indices\" not provided with triangle mesh shape"); return; }
+                if (!pp) { warn("Vertex positions \"P\" not provided with triangle mesh shape"); return; }
+                const Param* pS = ps.find("S", {"vector"});
+                const Param* pn = ps.find("N", {"normal"});
+                const bool useS = pS && (int)(pS->nums.size() / 3) == nv;
+                const bool useN = pn && (int)(pn->nums.size() / 3) == nv;
+                if (pS && !useS) warn("Number of \"S\"s for triangle mesh must match \"P\"s");
+                if (pn && !useN) warn("Number of \"N\"s for triangle mesh must match \"P\"s");
+                for (double v : pi->nums) {
+                    if (int(v) >= nv) {
+                        warn("trianglemesh has out of-bounds vertex index " + std::to_string(int(v)) + " (" +
+                             std::to_string(nv) + " \"P\" values were given");
+                        return;
+                    }
+                    idx.push_back(int(v));
+                }
+                idx.resize(idx.size() / 3 * 3);  // CreateTriangleMesh(..., nvi / 3, ...)
+                if (idx.empty()) return;           // zero triangles: no shapes
+                for (int k = 0; k < 3 * nv; ++k) P.push_back((float)pp->nums[k]);
+                if (useN) for (int k = 0; k < 3 * nv; ++k) N.push_back((float)pn->nums[k]);
+                if (useS) for (int k = 0; k < 3 * nv; ++k) S.push_back((float)pS->nums[k]);
+                if (useUV) for (int k = 0; k < 2 * nv; ++k) UV.push_back((float)puv->nums[k]);
             } else {
                 // CreatePLYMesh (plymesh.cpp:107-235); filename relative to the search directory
                 std::string f = ps.string1("filename", "");

@@ -212,7 +212,7 @@ struct Work {
             rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
             cap = n;
         }
-        spill.alloc(spill_threads * kCbSpillWords);  // k_trace_pt uses 64 words per lane, k_trace_cb 128
+        spill.alloc(spill_threads * 64);  // k_trace_pt: 64 words per lane (entries past its LDS rows)
         counts.alloc(8);
         stats.alloc(1);
     }
@@ -229,10 +229,21 @@ struct Work {
     }
 };
 
+// Restores a device as current when destroyed (dev < 0: nothing to restore).
+struct DeviceRestore {
+    int dev = -1;
+    ~DeviceRestore() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 }  // namespace pt
 
 struct pt_scene {
-    pt::DBuf<float4> nodes, prims, crec;
+    // declared first, destroyed last: gives the caller back its current device after every buffer and
+    // stream of the scene was freed with the scene's own device current
+    pt::DeviceRestore restore_dev;
+    pt::DBuf<float4> nodes, prims;
     pt::DBuf<pt_triangle> tris;
     pt::DBuf<float> P, N, S, UV, lfunc, lcdf, tri_area, perm_c0;
     pt::DBuf<pt::DevPlane> planes, pplanes;
@@ -270,9 +281,6 @@ struct pt_scene {
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
-    bool trace_cb = false;       // HBM-resident BVH under trace_persist 2: k_trace_cb (child-pair records; opt-in PT_TRACE_CB=1)
-    int cb_rows = 0;             // k_trace_cb: LDS stack rows (<= kCbStackRows), deeper entries spill
-    bool cb_spill = false;
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
@@ -289,7 +297,9 @@ struct pt_scene {
     std::vector<int> devices;  // ids[0..n) the scene was created for (primary first)
     ~pt_scene() {
         // replicas first (each makes its own device current), then this scene's streams and buffers are
-        // freed with its own device current
+        // freed with its own device current; restore_dev then makes the caller's device current again
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess) restore_dev.dev = cur;
         replicas.clear();
         (void)hipSetDevice(device);
     }
@@ -299,6 +309,12 @@ struct pt_scene {
 struct pt_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0, device = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the frame's reduce (pt_render_frame_dist), created once
+    ~pt_comm() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (comm) (void)ncclCommDestroy(comm);
+    }
 };
 
 namespace pt {
@@ -387,10 +403,6 @@ static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
     return sph ? k_trace_pt<false, false, true> : k_trace_pt<false, false, false>;
 }
 using TraceKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, int*, DevStats*);
-static TracePtKernel trace_cb_kernel(bool spill, bool sph) {
-    if (spill) return sph ? k_trace_cb<true, true> : k_trace_cb<true, false>;
-    return sph ? k_trace_cb<false, true> : k_trace_cb<false, false>;
-}
 static TraceKernel trace_kernel(bool lds, bool sph) {
     return lds ? (sph ? k_trace<true, true> : k_trace<true, false>) : (sph ? k_trace<false, true> : k_trace<false, false>);
 }
@@ -1081,6 +1093,21 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
     }
 }
 
+// Which traversal / shading kernel launch_trace / render_tiles run for this
+// scene (pt_scene_query PT_Q_TRACE_KERNEL / PT_Q_SHADE_KERNEL; the bench names
+// the kernel its roofline is for).
+static int trace_kernel_id(const pt_scene* s) {
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) return 3;
+    if (s->trace_persist == 2 && !s->trace_spill) return 2;
+    return s->trace_persist ? 1 : 0;
+}
+static int shade_variant_of(const pt_scene* s) { return s->shade_tab && s->shade_variant == 0 ? 5 : s->shade_variant; }
+static int shade_kernel_id(const pt_scene* s) {
+    if (s->hero) return s->hero_waves == 1 ? 7 : (s->hero_waves == 2 ? 8 : 9);
+    if (s->dev.integrator == PT_INTEGRATOR_DIRECT) return 6;
+    return shade_variant_of(s);
+}
+
 // One traversal launch over the nrays entries of ray queue rq (counts[0] holds
 // their number, counts[4] the persistent kernels' fetch cursor, zero): the
 // kernel this scene renders with (see create_scene_on).
@@ -1092,11 +1119,6 @@ static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
         hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
                            counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
-    } else if (s->trace_persist == 2 && s->trace_cb) {
-        // child-pair records from HBM: LDS stack rows of references + entry distances
-        const size_t lds = (size_t)2 * s->cb_rows * kTraceBlock * sizeof(int);
-        hipLaunchKernelGGL(trace_cb_kernel(s->cb_spill, s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
-                           counts + 0, counts + 4, s->refill_min, s->leaf_min_pt, s->cb_rows, w.spill.p, w.stats.p);
     } else if (s->trace_persist == 2 && !s->trace_spill) {
         // branch-reduced persistent traversal; LDS stack of depth+1 rows
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
@@ -1323,7 +1345,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 } else {
                     const ShadeKernel kshade =
                         direct ? k_shade_dl<kFtAll>
-                               : shade_kernel(s->shade_tab && s->shade_variant == 0 ? 5 : s->shade_variant, s->features);
+                               : shade_kernel(shade_variant_of(s), s->features);
                     hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
                                        pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }
@@ -1565,48 +1587,23 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
         s->trace_spill = sbound > s->stack_rows;
     }
     // kernel variants: LDS-resident BVH for small scenes (PT_TRACE_LDS=0 disables),
-    // shading register budget (PT_SHADE_VARIANT=3|4)
+    // shading register budget (PT_SHADE_VARIANT=0|3|5, below)
     const size_t scene_bytes = (2 * (size_t)s->dev.n_nodes + 3 * (size_t)s->dev.n_prims) * sizeof(float4);
     const char* e = std::getenv("PT_TRACE_LDS");
     s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                              ? scene_bytes : 0;
-    {   // child-pair records for an HBM-resident BVH (k_trace_cb), unless a leaf does not fit the encoding
-        const char* c = std::getenv("PT_TRACE_CB");
-        s->cb_rows = std::min(s->stack_rows, kCbStackRows);
-        s->cb_spill = sbound > s->cb_rows;
-        // opt-in (PT_TRACE_CB=1): C5 traces slower with it
-        s->trace_cb = s->lds_scene_bytes == 0 && !s->host_nodes.empty() && c && c[0] == '1' &&
-                      sbound <= s->cb_rows + kCbSpillWords / 2;
-        const auto& hn = s->host_nodes;
-        auto ref_of = [&](size_t c) -> int {
-            const LinearNode& m = hn[c];
-            if (m.nprims == 0) return (int)c;
-            if (m.nprims > 127 || m.offset < 0 || m.offset >= (1 << 24)) s->trace_cb = false;
-            return (int)(0x80000000u | (uint32_t)m.nprims << 24 | (uint32_t)m.offset);
-        };
-        if (s->trace_cb) {
-            std::vector<float4> rec(4 * hn.size(), make_float4(0.f, 0.f, 0.f, 0.f));
-            for (size_t i = 0; i < hn.size() && s->trace_cb; ++i) {
-                if (hn[i].nprims > 0) continue;
-                const size_t a = i + 1, b = (size_t)hn[i].offset;
-                const LinearNode &A = hn[a], &B = hn[b];
-                rec[4 * i] = make_float4(A.bmin[0], A.bmin[1], A.bmin[2], A.bmax[0]);
-                rec[4 * i + 1] = make_float4(A.bmax[1], A.bmax[2], __builtin_bit_cast(float, ref_of(a)),
-                                             __builtin_bit_cast(float, ref_of(b)));
-                rec[4 * i + 2] = make_float4(B.bmin[0], B.bmin[1], B.bmin[2], B.bmax[0]);
-                rec[4 * i + 3] = make_float4(B.bmax[1], B.bmax[2], __builtin_bit_cast(float, (int)hn[i].axis), 0.f);
-            }
-            s->dev.cb_root = ref_of(0);
-            if (s->trace_cb) {
-                s->crec.upload(rec);
-                s->dev.crec = s->crec.p;
-            }
-        }
-    }
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
-    if (v) s->shade_variant = std::atoi(v);
-    else if (s->shade_tab && !s->hero && s->features == kFtPortalOnly) {
+    if (v) {
+        s->shade_variant = std::atoi(v);
+        if (s->shade_variant != 0 && s->shade_variant != 3 && s->shade_variant != 5)
+            throw PtError(PT_ERR_INVALID_ARG, "PT_SHADE_VARIANT must be 0, 3 or 5");
+        // k_shade_w3 and k_shade_tab stage the scene tables in LDS: without room for them (tables larger
+        // than kTabLdsMax, or PT_SHADE_TAB=0) the launch's dynamic LDS holds only the Halton tables, so
+        // those builds would copy past their allocation -- take k_shade instead
+        if (!s->shade_tab) s->shade_variant = 0;
+        if (s->shade_variant == 3) s->shade_bpc = kShadeBpcW3;
+    } else if (s->shade_tab && !s->hero && s->features == kFtPortalOnly) {
         // the 3-waves-per-SIMD build of k_shade_tab when it needs no scratch (spills cost more than the
         // third wave gains), with the grid-stride loop sized for it (PT_SHADE_BPC overrides).  Only for
         // portal-only scenes: the MIS kernels' 3-wave build gives up the body prefetch (kLean), and with
@@ -1625,7 +1622,6 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,
                      s->trace_spill, s->lds_scene_bytes,
                      s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean ? "k_trace_lds"
-                     : s->trace_persist == 2 && s->trace_cb                                        ? "k_trace_cb"
                      : s->trace_persist == 2 && !s->trace_spill                                    ? "k_trace_nb"
                      : s->trace_persist                                                            ? "k_trace_pt"
                                                                                                    : "k_trace");
@@ -1733,6 +1729,8 @@ pt_status pt_scene_query(const pt_scene* s, int32_t key, int64_t* value) {
             case PT_Q_TRACE_LDS_BYTES: *value = (int64_t)s->lds_scene_bytes; break;
             case PT_Q_TRACE_SPILL: *value = s->trace_spill; break;
             case PT_Q_FEATURES: *value = s->features; break;
+            case PT_Q_TRACE_KERNEL: *value = trace_kernel_id(s); break;
+            case PT_Q_SHADE_KERNEL: *value = shade_kernel_id(s); break;
             default: throw PtError(PT_ERR_INVALID_ARG, "unknown pt_scene_query key");
         }
     });
@@ -1804,11 +1802,7 @@ pt_status pt_comm_create(int nranks, int rank, const uint8_t* id, pt_comm** out)
     });
 }
 
-void pt_comm_destroy(pt_comm* comm) {
-    if (!comm) return;
-    if (comm->comm) (void)ncclCommDestroy(comm->comm);
-    delete comm;
-}
+void pt_comm_destroy(pt_comm* comm) { delete comm; }
 
 pt_status pt_film_reduce(pt_comm* comm, const pt_scene* s, float* d_accum, int root, void* stream) {
     return guarded([&] {
@@ -1826,17 +1820,14 @@ pt_status pt_render_frame_dist(pt_scene* s, pt_comm* comm, float* d_accum, void*
         RenderResult r = render_tiles(s, comm->rank, comm->nranks, 0, s->spp, (float4*)d_accum, (hipStream_t)stream);
         // the frame's one collective, bracketed by events on its stream: reduce_ms is this rank's wait for
         // the slowest rank plus the transfer, the figure that tells tail imbalance from reduce cost
-        hipEvent_t e0, e1;
-        HIPCHK(hipEventCreate(&e0));
-        HIPCHK(hipEventCreate(&e1));
-        HIPCHK(hipEventRecord(e0, (hipStream_t)stream));
+        if (!comm->ev0) HIPCHK(hipEventCreate(&comm->ev0));
+        if (!comm->ev1) HIPCHK(hipEventCreate(&comm->ev1));
+        HIPCHK(hipEventRecord(comm->ev0, (hipStream_t)stream));
         NCCLCHK(ncclReduce(d_accum, d_accum, 4 * np, ncclFloat, ncclSum, 0, comm->comm, (hipStream_t)stream));
-        HIPCHK(hipEventRecord(e1, (hipStream_t)stream));
-        HIPCHK(hipEventSynchronize(e1));
+        HIPCHK(hipEventRecord(comm->ev1, (hipStream_t)stream));
+        HIPCHK(hipEventSynchronize(comm->ev1));  // returns after the reduce (pt.h)
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        HIPCHK(hipEventElapsedTime(&ms, comm->ev0, comm->ev1));
         fill_stats(r, stats);
         if (stats) stats->reduce_ms = ms;
     });

@@ -18,9 +18,5 @@ template __global__ void k_trace_lds<true>(PT_ARGS, uint32_t*, int, int, DevStat
 PT_PT(false, false, false) PT_PT(false, false, true) PT_PT(false, true, false) PT_PT(false, true, true)
 PT_PT(true, false, false) PT_PT(true, false, true) PT_PT(true, true, false) PT_PT(true, true, true)
 #undef PT_PT
-template __global__ void k_trace_cb<false, false>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);
-template __global__ void k_trace_cb<false, true>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);
-template __global__ void k_trace_cb<true, false>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);
-template __global__ void k_trace_cb<true, true>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);
 #undef PT_ARGS
 }  // namespace pt

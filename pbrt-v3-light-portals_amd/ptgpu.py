@@ -315,11 +315,19 @@ class Scene:
         """pt_set_pipelines: batches in flight (1 = one after the other)."""
         _check(lib().pt_set_pipelines(self._s, int(n)))
 
-    QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4}
+    QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4,
+                  "trace_kernel": 5, "shade_kernel": 6}
+    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds"}
+    SHADE_KERNELS = {0: "k_shade", 3: "k_shade_w3", 5: "k_shade_tab", 6: "k_shade_dl", 7: "k_shade_hero",
+                     8: "k_shade_hero_w2", 9: "k_shade_hero_w4"}
+
+    def kernel_names(self) -> Tuple[str, str]:
+        """(traversal kernel, shading kernel) a render of this scene launches."""
+        return self.TRACE_KERNELS[self.query("trace_kernel")], self.SHADE_KERNELS[self.query("shade_kernel")]
 
     def query(self, key: str) -> int:
         """pt_scene_query: a setting in effect (pipelines, batch_slots,
-        trace_lds_bytes, trace_spill, features)."""
+        trace_lds_bytes, trace_spill, features, trace_kernel, shade_kernel)."""
         v = ctypes.c_int64()
         _check(lib().pt_scene_query(self._s, self.QUERY_KEYS[key], ctypes.byref(v)))
         return v.value

@@ -13,6 +13,15 @@
                                     Transform, five axis-2 '+' portals, strategy projection, DirectLighting
   scenes/creeper/test00001.pbrt     scenes/blender/creeper/out/test00001.pbrt: path, trianglemesh emitter
   scenes/creeper/meshes/00001/*.ply their meshes (byte-identical copies)
+  scenes/lamp/test00001.pbrt        scenes/blender/lamp/out/test00001.pbrt: DiffuseAreaLight on an aaplane,
+                                    metal, DirectLighting (same meshes as lamp.pbrt)
+  scenes/spotlight/test00001.pbrt   scenes/blender/spotlight/out/test00001.pbrt: DirectLighting "one", two
+                                    diffuse trianglemesh lights, one of them an empty mesh ("point P" [])
+  scenes/spotlight/arealight.pbrt   scenes/blender/spotlight/out/arealight.pbrt: path maxdepth 10, aaplane
+                                    with the old loX/hiX parameters (lo = hi = 0, as in creeper)
+  scenes/window_portal_eq/test00001.pbrt  scenes/blender/window_portal_eq/out/test00001.pbrt: DirectLighting
+                                    "one", two diffuse lights
+  scenes/{spotlight,window_portal_eq}/meshes/00001/*.ply  the meshes they name (byte-identical copies)
 Scene files are renderer inputs (fixtures), not source; a provenance comment is
 prepended to each text file."""
 import os
@@ -26,11 +35,19 @@ TEXT = [("killeroo-simple.pbrt", "killeroo-simple.pbrt"),
         ("blender/lamp/out/lamp.pbrt", "lamp/lamp.pbrt"),
         ("blender/creeper/out/creeper.pbrt", "creeper/creeper.pbrt"),
         ("blender/creeper/out/sandbox.pbrt", "creeper/sandbox.pbrt"),
-        ("blender/creeper/out/test00001.pbrt", "creeper/test00001.pbrt")]
+        ("blender/creeper/out/test00001.pbrt", "creeper/test00001.pbrt"),
+        ("blender/lamp/out/test00001.pbrt", "lamp/test00001.pbrt"),
+        ("blender/spotlight/out/test00001.pbrt", "spotlight/test00001.pbrt"),
+        ("blender/spotlight/out/arealight.pbrt", "spotlight/arealight.pbrt"),
+        ("blender/window_portal_eq/out/test00001.pbrt", "window_portal_eq/test00001.pbrt")]
 BINARY = [("blender/lamp/out/meshes/00001/%s.ply" % m, "lamp/meshes/00001/%s.ply" % m)
           for m in ("Base_mat0", "Lampshade_mat0", "Leg_mat0", "Room_mat1", "Room_mat2")]
 BINARY += [("blender/creeper/out/meshes/00001/%s.ply" % m, "creeper/meshes/00001/%s.ply" % m)
            for m in ("Cube_mat0", "Ground_mat0", "creeper.001_mat0", "creeper_mat0")]
+BINARY += [("blender/spotlight/out/meshes/00001/%s.ply" % m, "spotlight/meshes/00001/%s.ply" % m)
+           for m in ("shade_mat1", "Suzanne_mat0")]
+BINARY += [("blender/window_portal_eq/out/meshes/00001/%s.ply" % m, "window_portal_eq/meshes/00001/%s.ply" % m)
+           for m in ("Cube_mat1", "Suzanne_mat0")]
 
 for rel, dst in TEXT:
     out = os.path.join(DST, dst)

@@ -28,24 +28,41 @@ def per_kernel(path):
     return d
 
 
+def source_hash_of(a):
+    if a.source_hash:
+        return a.source_hash
+    f = os.path.join(a.out, "source_hash.txt")
+    if os.path.exists(f):
+        return open(f).read().strip()
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    return bench.source_hash()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out")
     ap.add_argument("--round", default="r1")
+    ap.add_argument("--prof-dir", default="prof", help="subdirectory of --out with bench_kernel_stats.csv")
+    ap.add_argument("--fetch-dir", default="pmc_fetch")
+    ap.add_argument("--write-dir", default="pmc_write")
     ap.add_argument("--workload", required=True, help="bench config workload string the profile was taken on")
+    ap.add_argument("--source-hash", default="", help="bench.py source_hash() of the tree profiled "
+                    "(default: <out>/source_hash.txt, else this tree's)")
     a = ap.parse_args()
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copy(os.path.join(a.out, "prof", "bench_kernel_stats.csv"),
+    shutil.copy(os.path.join(a.out, a.prof_dir, "bench_kernel_stats.csv"),
                 os.path.join(prof, f"{a.round}_kernel_stats.csv"))
     stats = {}
-    for r in csv.DictReader(open(os.path.join(a.out, "prof", "bench_kernel_stats.csv"))):
+    for r in csv.DictReader(open(os.path.join(a.out, a.prof_dir, "bench_kernel_stats.csv"))):
         stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                           "total_ms": float(r["TotalDurationNs"]) / 1e6,
                                           "percent": float(r["Percentage"])}
-    fetch = per_kernel(os.path.join(a.out, "pmc_fetch", "fetch_counter_collection.csv"))
-    write = per_kernel(os.path.join(a.out, "pmc_write", "write_counter_collection.csv"))
+    fetch = per_kernel(os.path.join(a.out, a.fetch_dir, "fetch_counter_collection.csv"))
+    write = per_kernel(os.path.join(a.out, a.write_dir, "write_counter_collection.csv"))
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [0.0])
@@ -54,7 +71,7 @@ def main():
         wb = 1024.0 * sum(w) / len(w)
         kernels[k] = {"launches": len(f), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                       "hbm_bytes_per_launch": fb + wb, **({"stats": stats[k]} if k in stats else {})}
-    out = {"workload": a.workload,
+    out = {"workload": a.workload, "source_hash": source_hash_of(a),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "bytes = 2*FETCH_SIZE[KiB]*1024 + WRITE_SIZE[KiB]*1024 (gfx950 FETCH_SIZE half-count)",
            "kernels": kernels}

@@ -18,11 +18,14 @@ ap.add_argument("--out", default="gpurun_out")
 ap.add_argument("--round", default="r2")
 ap.add_argument("--workload", required=True)
 ap.add_argument("--args", default="--spp 16", help="bench args the passes ran with")
+ap.add_argument("--config", default="c2", help="bench --config the passes ran")
+ap.add_argument("--glob", default="pmc_sq*", help="pass directories under --out")
+ap.add_argument("--source-hash", default="", help="default: <out>/source_hash.txt, else this tree's")
 a = ap.parse_args()
 
 sums = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-for f in glob.glob(os.path.join(a.out, "pmc_sq*", "**", "*counter_collection.csv"), recursive=True):
+for f in glob.glob(os.path.join(a.out, a.glob, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         if not ("k_shade" in k or "k_trace" in k or "k_film" in k or "k_camera" in k):
@@ -30,7 +33,15 @@ for f in glob.glob(os.path.join(a.out, "pmc_sq*", "**", "*counter_collection.csv
         sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", ""))
 
-out = {"workload": a.workload, "bench_args": a.args,
+src = a.source_hash
+if not src and os.path.exists(os.path.join(a.out, "source_hash.txt")):
+    src = open(os.path.join(a.out, "source_hash.txt")).read().strip()
+if not src:
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    import bench
+    src = bench.source_hash()
+out = {"workload": a.workload, "config": a.config, "source_hash": src, "bench_args": a.args,
        "method": "rocprofv3 --pmc, two passes of 8 SQ counters each (scripts/gpu_pmc_sq.sh); sums over dispatches",
        "kernels": {}}
 for k, c in sums.items():

@@ -123,8 +123,6 @@ TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders 
     "k_trace_lds": {},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
-    "k_trace_cb": {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1"},
-    "k_trace_cb_spill": {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1", "PT_STACK_ROWS": "2"},
     "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
     "k_trace_pt_spill": {"PT_TRACE_PERSIST": "1", "PT_STACK_ROWS": "2", "PT_TRACE_LDS": "0"},
     "k_trace": {"PT_TRACE_PERSIST": "0"},
@@ -242,9 +240,7 @@ def test_tile_groups_batching_equal(variant):
 
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_CB": "1", "PT_STACK_ROWS": "3"}])
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
@@ -256,6 +252,43 @@ def test_trace_variants_bit_exact(variant, monkeypatch, env):
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst["node_visits"] == rst["node_visits"]
+
+
+SHADE_VARIANTS = [
+    {"PT_SHADE_VARIANT": "0"},                          # k_shade (scene tables from HBM)
+    {"PT_SHADE_VARIANT": "5"},                          # k_shade_tab, 2 waves per SIMD
+    {"PT_SHADE_VARIANT": "3"},                          # k_shade_w3 (MIS scenes: the kLean 3-wave build)
+    {"PT_SHADE_VARIANT": "3", "PT_SHADE_TAB": "0"},     # no table room: falls back to k_shade
+    {"PT_SHADE_VARIANT": "5", "PT_SHADE_TAB": "0"},
+]
+
+
+@pytest.mark.parametrize("scene", ["portal_cornell.pbrt", "portal_room.pbrt", "lamp/lamp.pbrt"])
+@pytest.mark.parametrize("env", SHADE_VARIANTS, ids=lambda e: "-".join("%s=%s" % kv for kv in e.items()))
+def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
+    """Every shading build PT_SHADE_VARIANT can select, on a portal-only scene
+    (C2), a portal + infinite-light MIS scene (C4) and the reference's lamp
+    scene (MIS over a diffuse aaplane + portal light), renders the oracle's
+    image bit for bit.  PT_SHADE_TAB=0 leaves no LDS room for the scene tables:
+    variants 3 / 5 then fall back to k_shade instead of copying past the
+    launch's LDS."""
+    from conftest import scene_variant
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    path = scene_variant(tmp_path, name=scene, res=(48, 32), spp=8)
+    hs, sc = _scene(path)
+    got, gst = sc.render()
+    ref, rst = pyoracle.render(hs.desc, nthreads=8)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k
+
+
+def test_shade_variant_rejects_unknown(variant, monkeypatch):
+    monkeypatch.setenv("PT_SHADE_VARIANT", "4")
+    hs = ptgpu.HostScene(variant(**MINI))
+    with pytest.raises(ptgpu.PtError, match="PT_SHADE_VARIANT"):
+        ptgpu.Scene(hs)
 
 
 def _bsdf_records(n, seed):
@@ -671,3 +704,21 @@ def test_film_pixel_lanes_match_oracle(tmp_path, monkeypatch, filt, spp):
     monkeypatch.setenv("PT_FILM_T", "0")
     old, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
     assert np.array_equal(old.view(np.uint32), got.view(np.uint32))
+
+
+def test_full_config_sparse_tiles_bit_exact():
+    """Parity at the benchmarked configuration: the C2 scene as benchmarked
+    (1920x1080 @256 spp, path maxdepth 5, the default 64 M-slot batches and
+    two pipelines) on the tiles t % 400 == 0 spread over the whole frame,
+    against the oracle's film of the same tiles (SamplerIntegrator::Render,
+    integrator.cpp:526-637) -- bit-identical film and identical counters."""
+    hs = ptgpu.HostScene(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scenes",
+                                      "portal_cornell.pbrt"))
+    sc = ptgpu.Scene(hs)
+    assert sc.film_size() == (1920, 1080)
+    got, gst = sc.render_accum(0, 400)
+    ref, rst = pyoracle.render_accum(hs.desc, nthreads=16, tile_offset=0, tile_stride=400)
+    assert gst["samples"] == rst["samples"] == 21 * 256 * 256
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+        assert gst[k] == rst[k], k

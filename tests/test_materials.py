@@ -87,26 +87,26 @@ def _cosine_hemisphere(u0, u1):
     return np.array([r * math.cos(phi), r * math.sin(phi), math.sqrt(max(0.0, 1 - u0))])
 
 
-@pytest.mark.parametrize("rough", ['"float roughness" [0.5] "bool remaproughness" "false"',
-                                   '"float uroughness" [0.3] "float vroughness" [0.15] "bool remaproughness" "false"',
-                                   '"float roughness" [0.3] "bool remaproughness" "false"'])
-def test_microfacet_sampling_chi2(tmp_path, rough):
-    """BSDFSampling.TR_VA_0p5 / TR_VA_0p3_0p15 / TR_VA_0p3 (bsdfs.cpp:493-546):
-    histogram of Sample_f directions vs N * integral of Pdf per (theta, phi)
-    cell, chi^2 with low-frequency cells merged (CHI2_MINFREQ 5), significance
-    0.01 Bonferroni-corrected over the runs."""
+def bsdf_chi2(eval_fn, runs=3, n=400000, seed=7):
+    """TestBSDF (src/tests/bsdfs.cpp:371-438): per run a cosine-distributed wo,
+    the histogram of BSDF::Sample_f directions (theta x phi = 10 x 20 cells,
+    FrequencyTable) against N * the integral of BSDF::Pdf over each cell
+    (IntegrateFrequencyTable; midpoint rule here), chi^2 with the cells of
+    expected frequency < CHI2_MINFREQ = 5 pooled, significance 0.01
+    Bonferroni-corrected over the runs (Chi2Test).  eval_fn: (n, 8) records
+    wo, wi, u0, u1 -> (n, 8) f, pdf, sampled wi, sampled pdf (the oracle's
+    bsdf_batch or the device's pt_debug_bsdf)."""
     from scipy.stats import chi2
-    hs = ptgpu.HostScene(metal_scene(tmp_path, rough=rough, res=(8, 8), spp=1))
-    mat = _metal_index(hs)
-    rng = np.random.default_rng(7)
-    theta_res, phi_res, n, runs = 10, 20, 400000, 3
+    rng = np.random.default_rng(seed)
+    theta_res, phi_res = 10, 20
     sig = 1.0 - (1.0 - 0.01) ** (1.0 / runs)
+    pvals = []
     for run in range(runs):
         wo = _cosine_hemisphere(*rng.random(2)).astype(np.float32)
         rec = np.zeros((n, 8), np.float32)
         rec[:, 0:3] = wo
         rec[:, 6:8] = rng.random((n, 2), dtype=np.float32) * F32(0.99999994)
-        out = pyoracle.bsdf_batch(hs.desc, mat, rec)
+        out = eval_fn(rec)
         ok = (out[:, 0:3].max(axis=1) > 0) & (out[:, 7] > 0)
         wi = out[ok, 4:7].astype(np.float64)
         th = np.arccos(np.clip(wi[:, 2], -1, 1)) * theta_res / math.pi
@@ -124,7 +124,7 @@ def test_microfacet_sampling_chi2(tmp_path, rough):
         q = np.zeros((len(dirs), 8), np.float32)
         q[:, 0:3] = wo
         q[:, 3:6] = dirs
-        pdf = pyoracle.bsdf_batch(hs.desc, mat, q)[:, 3].astype(np.float64).reshape(theta_res * k, phi_res * k)
+        pdf = eval_fn(q)[:, 3].astype(np.float64).reshape(theta_res * k, phi_res * k)
         cell = (math.pi / (theta_res * k)) * (2 * math.pi / (phi_res * k))
         dens = pdf * np.sin(T) * cell
         exp = dens.reshape(theta_res, k, phi_res, k).sum(axis=(1, 3)).reshape(-1) * n
@@ -143,6 +143,53 @@ def test_microfacet_sampling_chi2(tmp_path, rough):
             dof += 1
         pval = 1.0 - chi2.cdf(stat, dof - 1)
         assert pval > sig, (run, stat, dof, pval)
+        pvals.append(pval)
+    return pvals
+
+
+@pytest.mark.parametrize("rough", ['"float roughness" [0.5] "bool remaproughness" "false"',
+                                   '"float uroughness" [0.3] "float vroughness" [0.15] "bool remaproughness" "false"',
+                                   '"float roughness" [0.3] "bool remaproughness" "false"'])
+def test_microfacet_sampling_chi2(tmp_path, rough):
+    """BSDFSampling.TR_VA_0p5 / TR_VA_0p3_0p15 / TR_VA_0p3 (bsdfs.cpp:493-546)."""
+    hs = ptgpu.HostScene(metal_scene(tmp_path, rough=rough, res=(8, 8), spp=1))
+    mat = _metal_index(hs)
+    bsdf_chi2(lambda rec: pyoracle.bsdf_batch(hs.desc, mat, rec))
+
+
+LAMBERT_BOX = '''
+AttributeBegin
+  Material "matte" "rgb Kd" [1 1 1] "float sigma" [0]
+  Shape "trianglemesh" "point P" [150 0 150  400 0 150  400 200 300  150 200 300] "integer indices" [0 1 2 0 2 3]
+AttributeEnd
+'''
+
+
+def _lambert(tmp_path):
+    hs = ptgpu.HostScene(scene_variant(tmp_path, extra=[("WorldEnd", LAMBERT_BOX + "WorldEnd")], res=(8, 8), spp=1))
+    idx = [i for i, m in enumerate(hs.materials()) if m.kind == 1 and list(m.kd) == [1.0, 1.0, 1.0]]
+    assert idx, "no Kd = 1 matte material"
+    return hs, idx[0]
+
+
+def test_lambertian_sampling_chi2(tmp_path):
+    """BSDFSampling.Lambertian (bsdfs.cpp:440-443, 485): LambertianReflection
+    with Kd = 1 (MatteMaterial with sigma 0 makes exactly that BSDF,
+    matte.cpp:40-55) -- 5 runs of 1 M samples, as the reference test."""
+    hs, mat = _lambert(tmp_path)
+    bsdf_chi2(lambda rec: pyoracle.bsdf_batch(hs.desc, mat, rec), runs=5, n=1000000)
+
+
+@pytest.mark.gpu
+def test_lambertian_sampling_chi2_device(tmp_path):
+    """The same test through the device's BSDF (pt_debug_bsdf): the chi^2
+    test passes, and every record is bit-identical to the oracle's."""
+    hs, mat = _lambert(tmp_path)
+    sc = ptgpu.Scene(hs)
+    bsdf_chi2(lambda rec: sc.debug_bsdf(mat, rec), runs=5, n=1000000)
+    rec = np.random.default_rng(3).random((4096, 8), dtype=np.float32)
+    rec[:, 0:6] -= F32(0.5)
+    assert np.array_equal(sc.debug_bsdf(mat, rec).view(np.uint32), pyoracle.bsdf_batch(hs.desc, mat, rec).view(np.uint32))
 
 
 # ---- PLY meshes (shapes/plymesh.cpp) ---------------------------------------------------------

@@ -15,7 +15,20 @@ verbatim by scripts/import_reference_scenes.py into scenes/creeper/):
   portal pdf with the untransformed Normal() (aaportal.cpp:82), InFront in
   light object space (aaportal.cpp:98), WorldToObject applied to the sampled
   object-space point (aaportal.cpp:154);
-* test00001.pbrt -- path, a trianglemesh emitter with normals and st.
+* test00001.pbrt -- path, a trianglemesh emitter with normals and st;
+
+and (round 4) the reference's other renderable blender scenes:
+
+* lamp/test00001.pbrt -- DirectLighting over the lamp meshes, a DiffuseAreaLight
+  on an aaplane given with the old loX/hiX parameters (CreateAAPlaneShape reads
+  only "point lo"/"point hi", plane.cpp:117-128, so lo = hi = 0: the light is
+  never hit nor sampled and the image is black, as the reference renders it);
+* spotlight/test00001.pbrt -- DirectLighting "one" with two diffuse trianglemesh
+  lights, one of them an empty mesh ("point P" [] ... "integer indices" []):
+  CreateTriangleMeshShape makes zero triangles, so that AreaLightSource yields
+  no light (triangle.cpp:911-971, api.cpp MakeShapes);
+* spotlight/arealight.pbrt -- path maxdepth 10, the same old-parameter aaplane;
+* window_portal_eq/test00001.pbrt -- DirectLighting "one", two diffuse lights.
 
 GPU tests render each as written and as `path` (x strategies) through the C
 ABI and compare with the oracle bit for bit, ray / node / prim counters
@@ -74,6 +87,83 @@ def test_reference_scenes_load():
     hs = ptgpu.HostScene(os.path.join(SCENES, "creeper", "test00001.pbrt"))
     d = ptgpu.scene_desc(hs)
     assert (d.n_triangles, d.n_lights, d.integrator.kind) == (4, 2, 0)
+
+
+ROUND4 = {  # scene: (tris, planes, lights, integrator kind, maxdepth, spp)
+    "lamp/test00001.pbrt": (324, 1, 1, 1, 100, 20),
+    "spotlight/test00001.pbrt": (3964, 0, 2, 1, 3, 25),
+    "spotlight/arealight.pbrt": (3962, 1, 1, 0, 10, 10),
+    "window_portal_eq/test00001.pbrt": (3962, 0, 2, 1, 5, 25),
+}
+
+
+@pytest.mark.parametrize("scene", sorted(ROUND4))
+def test_round4_reference_scenes_load(scene):
+    """The scenes load as the reference parses them: the empty trianglemesh
+    under spotlight's first AreaLightSource gives no shape and no light (two
+    lights, not three)."""
+    d = ptgpu.scene_desc(ptgpu.HostScene(os.path.join(SCENES, scene)))
+    got = (d.n_triangles, d.n_planes, d.n_lights, d.integrator.kind, d.integrator.max_depth, d.sampler.spp)
+    assert got == ROUND4[scene]
+
+
+def _mesh_scene(tmp_path, shape, light=True):
+    """A one-emitter room (the furnace cube) plus `shape` under its own
+    AreaLightSource: what CreateTriangleMeshShape's error paths leave."""
+    from conftest import furnace_scene
+    txt = open(furnace_scene(tmp_path, res=8, spp=4, maxdepth=3)).read()
+    add = ("AttributeBegin\n" + ('  AreaLightSource "diffuse" "rgb L" [4 4 4]\n' if light else "") +
+           "  " + shape + "\nAttributeEnd\n")
+    txt = txt.replace("WorldEnd", add + "WorldEnd")
+    p = os.path.join(str(tmp_path), "mesh_%d.pbrt" % (abs(hash(shape)) % 10 ** 8))
+    open(p, "w").write(txt)
+    return p
+
+
+TRI = '"point P" [0 0 0.5  0.2 0 0.5  0 0.2 0.5]'
+
+
+@pytest.mark.parametrize("shape,ntris", [
+    ('Shape "trianglemesh" "point P" [] "normal N" [] "float st" [] "integer indices" []', 0),  # empty: no shapes
+    ('Shape "trianglemesh" ' + TRI, 0),                                # no indices: Error, no shapes
+    ('Shape "trianglemesh" "integer indices" [0 1 2]', 0),             # no P: Error, no shapes
+    ('Shape "trianglemesh" ' + TRI + ' "integer indices" [0 1 3]', 0),  # index past the last vertex
+    ('Shape "trianglemesh" ' + TRI + ' "integer indices" [0 1 2 1]', 1),  # nvi / 3 triangles
+    ('Shape "trianglemesh" ' + TRI + ' "integer indices" [0 1 2] "float uv" [0 0 1 0]', 1),  # too few uv
+    ('Shape "trianglemesh" ' + TRI + ' "integer indices" [0 1 2] "normal N" [0 0 1]', 1),    # N count mismatch
+    ('Shape "trianglemesh" "point P" [0 0 0.5  0.2 0 0.5  0 0.2 0.5  9] "integer indices" [0 1 2]', 1),  # P excess
+])
+def test_trianglemesh_error_contract(tmp_path, shape, ntris):
+    """CreateTriangleMeshShape (triangle.cpp:911-971): Error() and no shapes for
+    missing P / indices or an out-of-range index, the scene renders on; a uv
+    array with fewer entries than P, or an N / S array of another length, is
+    discarded; excess point values and a trailing partial index triple are
+    ignored (parser.cpp:603-615, CreateTriangleMesh(nvi / 3)).  An emitting
+    mesh of zero triangles adds no light (MakeShapes makes one
+    DiffuseAreaLight per shape)."""
+    hs = ptgpu.HostScene(_mesh_scene(tmp_path, shape))
+    d = ptgpu.scene_desc(hs)
+    assert d.n_triangles == 12 + ntris
+    assert d.n_lights == 12 + ntris
+    if ntris:  # the discarded arrays: no uv / normals / tangents on the triangle (pt_triangle: 6 words)
+        words = ctypes.cast(d.triangles, ctypes.POINTER(ctypes.c_uint32))
+        assert words[12 * 6 + 5] & (4 | 8 | 16) == 0
+    img, st = pyoracle.render(hs.desc, nthreads=4)
+    assert np.isfinite(img).all() and st["samples"] == 8 * 8 * 4
+
+
+def test_empty_emitter_mesh_adds_no_light(tmp_path):
+    """An empty trianglemesh under an AreaLightSource (spotlight/test00001.pbrt)
+    leaves the scene exactly as if the attribute block were absent: same
+    lights, same image, same ray counts (oracle)."""
+    a = ptgpu.HostScene(_mesh_scene(tmp_path, 'Shape "trianglemesh" "point P" [] "integer indices" []'))
+    from conftest import furnace_scene
+    b = ptgpu.HostScene(furnace_scene(tmp_path, res=8, spp=4, maxdepth=3))
+    assert ptgpu.scene_desc(a).n_lights == ptgpu.scene_desc(b).n_lights == 12
+    ia, sa = pyoracle.render(a.desc, nthreads=4)
+    ib, sb = pyoracle.render(b.desc, nthreads=4)
+    assert np.array_equal(_bits(ia), _bits(ib))
+    assert sa == sb
 
 
 def test_creeper_degenerate_plane_light_contributes_nothing(tmp_path):
@@ -202,3 +292,21 @@ def test_portal_count_cap_device(tmp_path):
     with pytest.raises(ptgpu.PtError) as e:
         ptgpu.Scene(hs)
     assert e.value.status == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", sorted(ROUND4))
+def test_round4_reference_scenes_as_written_match_oracle(tmp_path, scene):
+    """The reference's lamp / spotlight / window_portal_eq scenes as written
+    (DirectLighting "one" and path maxdepth 10, the scene's film and spp),
+    bit-identical to the oracle with identical counters."""
+    _gpu_vs_oracle(scene_variant(tmp_path, name=scene))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", sorted(ROUND4))
+def test_round4_reference_scenes_as_path_match_oracle(tmp_path, scene):
+    """The same scenes as PathIntegrator maxdepth 5."""
+    extra = [('Integrator "directlighting"', 'Integrator "path"'), ('"integer maxdepth" [10]', '"integer maxdepth" [5]'),
+             ('"integer maxdepth" [100]', '"integer maxdepth" [5]'), ('"integer maxdepth" [3]', '"integer maxdepth" [5]')]
+    _gpu_vs_oracle(scene_variant(tmp_path, name=scene, spp=8, extra=extra))
