@@ -165,27 +165,45 @@ __host__ __device__ inline TabLayout tab_layout(int n_prims, int n_mats, int n_l
     return t;
 }
 
-// Per-path SoA state for one batch of nslots camera samples.
+// Per-path state for one batch of nslots camera samples, as per-slot records:
+// a path step's fields share a sector instead of one 4-B field per sector
+// (the path queue is compacted every bounce, so a wave's slots are spread).
+//   head  16 B  {st (kSt* bits, NEE flags at kStNfShift), hit, hitA, hitB}: the
+//               step's first load (what it reads next); the trace kernels write
+//               the hit words
+//   body  32 B  {L.xyz, hidx} {beta.xyz, etaScale}
+//   nee   64 B  the deferred EstimateDirect payload (kNee* offsets)
+//   ray / rayA / rayB  32 B  {o.xyz, d.x} {d.yz, tMax, 0} (kernels.hip load_ray)
 struct DevPaths {
     int n;
-    uint32_t* hidx;     // Halton index of the sample
+    uint4* head;        // n
+    float4* body;       // 2n
     float2* pfilm;      // CameraSample::pFilm
-    float* L;           // 3n
-    float* beta;        // 3n
-    float* eta;         // n
-    uint32_t* st;       // n: packed state, see kSt* below
-    float* ray;         // 8n continuation ray: 32-B record per slot {o.xyz, d.x} {d.yz, tMax, 0} (kernels.hip load_ray)
-    int* hit;           // n
+    float* ray;         // 8n continuation ray
     float* rayA;        // 8n NEE ray A (MIS shadow ray: its tMax), same record
-    int* hitA;          // n
     float* rayB;        // 8n NEE ray B, same record
-    int* hitB;          // n
-    float* nee;         // kNee * n payload
+    float* nee;         // kNee floats per slot
     // DirectLightingIntegrator only (null otherwise): see kDl* below
     int* dli;           // kDlInts * n
     float* dlf;         // kDlFloats * n
     float* dlframe;     // kDlFrame * frames * n: the specular recursion stack
 };
+
+// head / body words of a slot
+constexpr int kHdSt = 0, kHdHit = 1, kHdHitA = 2, kHdHitB = 3;
+constexpr int kBdL = 0, kBdHidx = 3, kBdBeta = 4, kBdEta = 7;
+__device__ __forceinline__ uint32_t* st_word(const DevPaths& ps, uint32_t slot) {
+    return reinterpret_cast<uint32_t*>(ps.head) + (4u * slot);
+}
+__device__ __forceinline__ int* hit_word(const DevPaths& ps, uint32_t slot, int k) {
+    return reinterpret_cast<int*>(ps.head) + (4u * slot + (uint32_t)k);
+}
+__device__ __forceinline__ float* body_word(const DevPaths& ps, uint32_t slot, int k) {
+    return reinterpret_cast<float*>(ps.body) + (8u * slot + (uint32_t)k);
+}
+__device__ __forceinline__ uint32_t hidx_of(const DevPaths& ps, uint32_t slot) {
+    return __float_as_uint(*body_word(ps, slot, kBdHidx));
+}
 
 // DirectLightingIntegrator per-sample state (kernels.hip shade_dl).
 // Integer fields (dli[k * n + slot]):
@@ -215,26 +233,29 @@ constexpr int kFrPdf = 14;   // pdf
 constexpr int kFrPhase = 15; // 0: reflection child pending (transmission next), 1: transmission child
 constexpr int kDlFrame = 16;
 
-// st bits
-constexpr uint32_t kStDimMask = 0xffffu;
-constexpr uint32_t kStBounceShift = 16;      // 8 bits
-constexpr uint32_t kStSpecular = 1u << 24;
-constexpr uint32_t kStCont = 1u << 25;       // continuation ray pending
-constexpr uint32_t kStNee = 1u << 26;        // NEE payload pending
-constexpr uint32_t kStDimOverflow = 1u << 27;
+// st bits: sampler dimension (PrimeTableSize 1000 < 4096), bounces, flags,
+// and the pending NEE payload's kNf* flags
+constexpr uint32_t kStDimMask = 0xfffu;
+constexpr uint32_t kStBounceShift = 12;      // 8 bits
+constexpr uint32_t kStSpecular = 1u << 20;
+constexpr uint32_t kStCont = 1u << 21;       // continuation ray pending
+constexpr uint32_t kStNee = 1u << 22;        // NEE payload pending
+constexpr uint32_t kStDimOverflow = 1u << 23;
+constexpr uint32_t kStNfShift = 24;          // kNf* << 24
+constexpr uint32_t kStNfMask = 0x3fu << kStNfShift;
 
-// NEE payload layout (floats, stride n)
+// NEE payload: kNee floats per slot (ps.nee[kNee * slot + k]), four 16-B
+// quarters read as the resolve needs them
 constexpr int kNee = 16;
-constexpr int kNeeBeta = 0;    // 3: beta at the vertex
-constexpr int kNeeF = 3;       // 3: f*|cos| (portal kinds) or c1 (MIS light part)
-constexpr int kNeePdf = 6;     // portal-kind sampling pdf
-constexpr int kNeeLi = 7;      // 3: Li fallback on miss (portal kinds) / f2 (MIS)
-constexpr int kNeeSw = 10;     // MIS scattering weight
-constexpr int kNeeSpdf = 11;   // MIS scattering pdf
-constexpr int kNeeLpdf = 12;   // light selection pdf (UniformSampleOneLight)
+constexpr int kNeeBeta = 0;    // 3: beta at the vertex                              | quarter 0
+constexpr int kNeeLpdf = 3;    // light selection pdf (UniformSampleOneLight)
+constexpr int kNeeF = 4;       // 3: f*|cos| (portal kinds) or c1 (MIS light part)   | quarter 1
+constexpr int kNeePdf = 7;     // portal-kind sampling pdf
+constexpr int kNeeLi = 8;      // 3: Li fallback on miss (portal kinds) / f2 (MIS)   | quarter 2
+constexpr int kNeeSw = 11;     // MIS scattering weight
+constexpr int kNeeSpdf = 12;   // MIS scattering pdf                                 | quarter 3
 constexpr int kNeePortalPdf = 13;
 constexpr int kNeeLight = 14;  // light index (int bits)
-constexpr int kNeeFlags = 15;  // kNf* (int bits)
 
 constexpr uint32_t kNfPortal = 1u;     // portal-light estimator (ray A closest)
 constexpr uint32_t kNfMis = 2u;        // standard MIS (ray A shadow, ray B closest)

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void k_hero_init(DevScene sc, DevHero h, DevPa
 {
     const uint32_t N = (uint32_t)ps.n;
     for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < total; slot += gridDim.x * blockDim.x) {
-        const float uw = halton_dim(sc, ps.hidx[slot], sc.wvl_dim);
+        const float uw = halton_dim(sc, hidx_of(ps, slot), sc.wvl_dim);
         for (int i = 0; i < 4; ++i) {
             // rotateValue: fmod(sample + i / 4, 1.0) in double (hero.cpp:45-47)
             const float s = (float)fmod((double)(uw + (float)i / (float)4), 1.0);
@@ -453,7 +453,7 @@ template <int kFt>
 __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, const DevPaths& ps, const DevHeroPaths& hp,
                           uint32_t slot, RayList* rays, bool* overflow, uint32_t* ab) {
     const uint32_t N = (uint32_t)ps.n;
-    uint32_t st = ps.st[slot];
+    uint32_t st = *st_word(ps, slot);
     float* Lg = hp.L + hbin_at(N, slot, 0);
     float* Bg = hp.beta + hbin_at(N, slot, 0);
     float* Ng = hp.nee + hbin_at(N, slot, 0);
@@ -468,7 +468,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     auto count = [&]() { *ab += sb + 4 * kNS * (uint32_t)__builtin_popcount(tch); };
     if (st & kStNee) {
         if (hf & kHfPend) sb += 4;  // hitA
-        if ((hf & kHfPend) && ps.hitA[slot] == 0)
+        if ((hf & kHfPend) && *hit_word(ps, slot, kHdHitA) == 0)
             #pragma unroll 1
             for (int i0 = 0; i0 < kNS; i0 += kG) {
                 float l[kG], x[kG];
@@ -511,13 +511,13 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     };
     if (!(st & kStCont)) {
         H[kHsFlags * BS] = __uint_as_float(hf);
-        ps.st[slot] = st;
+        *st_word(ps, slot) = st;
         finish();
         count();
         return;
     }
     st &= ~kStCont;
-    Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+    Dims dm{&sc, hidx_of(ps, slot), (int)(st & kStDimMask), false};
     int bounces = (int)((st >> kStBounceShift) & 0xffu);
     float wvls[4], pathWvlPdf[4], prev[4];
     int wvlIdx[4];
@@ -533,7 +533,7 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     Ray ray = load_ray(ps.ray, slot, kInf);
     sb += 4 + 56 + 24 + 4;  // hidx, H wavelengths / pdfs / etaScale / bsdfPdf, ray, hit
     const V3 rayO = ray.o;
-    const int hpr = ps.hit[slot];
+    const int hpr = *hit_word(ps, slot, kHdHit);
     SurfHit si;
     const bool found = hpr >= 0 && surface_at<Ft<kFt>::sph>(sc, hpr, ray, &si);
     // Lo += beta * Le, weighted (hero_path.cpp:84-104, hero_path_mis.cpp:120-166)
@@ -841,10 +841,10 @@ __device__ __forceinline__ void hero_step(const DevScene& sc, const DevHero& h, 
     }
     if (cont) st |= kStCont;
     if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
-    st = (st & ~(kStDimMask | (0xffu << kStBounceShift))) | ((uint32_t)dm.dim & kStDimMask) |
-         ((uint32_t)bounces << kStBounceShift);
+    st = (st & ~(kStDimMask | (0xffu << kStBounceShift))) | (uint32_t)min(dm.dim, (int)kStDimMask) |
+         ((uint32_t)(bounces & 0xff) << kStBounceShift);
     H[kHsFlags * BS] = __uint_as_float(hf);
-    ps.st[slot] = st;
+    *st_word(ps, slot) = st;
     if (!(st & (kStCont | kStNee))) finish();
     sb += 4 * (rays->n + ((st & (kStCont | kStNee)) ? 1u : 0u));  // ray / path queue entries written
     count();
@@ -868,7 +868,7 @@ __device__ __forceinline__ void shade_hero_batch(const DevScene& sc, const DevHe
         if (i < n) {
             slot = pq[i];
             hero_step<kFt>(sc, h, ps, hp, slot, &rays, &overflow, &ab);
-            keep = (ps.st[slot] & (kStCont | kStNee)) != 0;
+            keep = (*st_word(ps, slot) & (kStCont | kStNee)) != 0;
         }
         wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
     }

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
         if (kind == kRayShadow) {
             Ray r = load_ray(ps.rayA, slot);
             int h = traverse<true, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
-            ps.hitA[slot] = h >= 0 ? 1 : 0;
+            *hit_word(ps, slot, kHdHitA) = h >= 0 ? 1 : 0;
             ++nsh;
         } else {
             Ray r;
@@ -291,9 +291,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace(DevScene sc, DevPaths ps,
             else if (kind == kRayA) r = load_ray(ps.rayA, slot, kInf);
             else r = load_ray(ps.rayB, slot, kInf);
             int h = traverse<false, kSph>(sc, bnodes, bprims, r, stk, myspill, &nodes, &prims);
-            if (kind == kRayCont) ps.hit[slot] = h;
-            else if (kind == kRayA) ps.hitA[slot] = h;
-            else ps.hitB[slot] = h;
+            if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = h;
+            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = h;
+            else *hit_word(ps, slot, kHdHitB) = h;
             ++ncl;
         }
     }
@@ -405,10 +405,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                         cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
                         active = sc.n_nodes > 0;  // empty scene: every ray misses
                         if (!active) {
-                            if (kind == kRayShadow) ps.hitA[slot] = 0;
-                            else if (kind == kRayCont) ps.hit[slot] = -1;
-                            else if (kind == kRayA) ps.hitA[slot] = -1;
-                            else ps.hitB[slot] = -1;
+                            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
+                            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = -1;
+                            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
+                            else *hit_word(ps, slot, kHdHitB) = -1;
                         }
                         if (kind == kRayShadow) ++nsh; else ++ncl;
                     }
@@ -493,10 +493,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
             }
         }
         if (done) {
-            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
-            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
-            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
-            else ps.hitB[slot] = hitPrim;
+            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
+            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
+            else *hit_word(ps, slot, kHdHitB) = hitPrim;
             active = false;
         }
     }
@@ -595,10 +595,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
                         cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
                         active = sc.n_nodes > 0;  // empty scene: every ray misses
                         if (!active) {
-                            if (kind == kRayShadow) ps.hitA[slot] = 0;
-                            else if (kind == kRayCont) ps.hit[slot] = -1;
-                            else if (kind == kRayA) ps.hitA[slot] = -1;
-                            else ps.hitB[slot] = -1;
+                            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
+                            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = -1;
+                            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
+                            else *hit_word(ps, slot, kHdHitB) = -1;
                         }
                         if (kind == kRayShadow) ++nsh; else ++ncl;
                     }
@@ -676,10 +676,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
             }
         }
         if (done) {
-            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
-            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
-            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
-            else ps.hitB[slot] = hitPrim;
+            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
+            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
+            else *hit_word(ps, slot, kHdHitB) = hitPrim;
             active = false;
         }
     }
@@ -833,10 +833,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                     cur = node0; sp = sbase; hitPrim = -1; leafPos = 0; leafEnd = 0;
                     active = sc.n_nodes > 0;  // empty scene: every ray misses
                     if (!active) {
-                        if (kind == kRayShadow) ps.hitA[slot] = 0;
-                        else if (kind == kRayCont) ps.hit[slot] = -1;
-                        else if (kind == kRayA) ps.hitA[slot] = -1;
-                        else ps.hitB[slot] = -1;
+                        if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
+                        else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = -1;
+                        else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
+                        else *hit_word(ps, slot, kHdHitB) = -1;
                     }
                     nrays += kind == kRayShadow ? 0x10000u : 1u;
                 }
@@ -909,10 +909,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             }
         }
         if (done) {
-            if (kind == kRayShadow) ps.hitA[slot] = hitPrim >= 0 ? 1 : 0;
-            else if (kind == kRayCont) ps.hit[slot] = hitPrim;
-            else if (kind == kRayA) ps.hitA[slot] = hitPrim;
-            else ps.hitB[slot] = hitPrim;
+            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
+            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
+            else *hit_word(ps, slot, kHdHitB) = hitPrim;
             active = false;
         }
     }
@@ -960,14 +960,12 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
         float lx = 0.5f, ly = 0.5f;
         if (sc.lens_radius > 0) { lx = halton_dim(sc, idx, 3); ly = halton_dim(sc, idx, 4); }
         const Ray r = camera_ray(sc, fx, fy, lx, ly);
-        ps.hidx[slot] = idx;
         ps.pfilm[slot] = make_float2(fx, fy);
-        ps.L[slot] = 0.f; ps.L[N + slot] = 0.f; ps.L[2 * N + slot] = 0.f;
-        ps.beta[slot] = 1.f; ps.beta[N + slot] = 1.f; ps.beta[2 * N + slot] = 1.f;
-        ps.eta[slot] = 1.f;
+        ps.body[2 * (size_t)slot] = make_float4(0.f, 0.f, 0.f, __uint_as_float(idx));  // L = 0, hidx
+        ps.body[2 * (size_t)slot + 1] = make_float4(1.f, 1.f, 1.f, 1.f);              // beta = 1, etaScale = 1
         // dims 0-4 (pFilm, time, pLens) and the wvl dimension consumed; with sample
         // arrays Get1D jumps over [5, arrayEndDim) for wvl (sampler.cpp:180-184)
-        ps.st[slot] = (uint32_t)(sc.wvl_dim + 1) | kStCont;
+        ps.head[slot] = make_uint4((uint32_t)(sc.wvl_dim + 1) | kStCont, 0u, 0u, 0u);
         if (ps.dli) {
             ps.dli[kDlD * N + slot] = 0;
             ps.dli[kDlAoff * N + slot] = 0;
@@ -1050,28 +1048,38 @@ struct NeeIn {
 };
 // Only the fields the resolve of this payload reads (flags fl, the hits hA /
 // hB of rays A and B): what nee_value touches under the same conditions.
+// The payload is one 64-B record per slot: each quarter a resolve needs is one
+// 16-B load.
+// kMis: the scene has lights the MIS branch samples (Ft::mis).
+template <bool kMis = true>
 __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uint32_t fl, int hA) {
-    const uint32_t N = (uint32_t)ps.n;
-    const float* nee = ps.nee;
+    const float4* q = reinterpret_cast<const float4*>(ps.nee) + 4u * slot;
     NeeIn in{s3(0.f), s3(0.f), s3(0.f), 0.f, 0.f, 1.f, 0, Ray{v3(0, 0, 0), v3(0, 0, 1), kInf}};
     const bool portalA = (fl & kNfPortal) && (fl & kNfA);
-    const bool misB = !(fl & kNfPortal) && (fl & kNfMis) && (fl & kNfB);
-    const bool mis = !(fl & kNfPortal) && (fl & kNfMis);
-    in.beta = s3(nee[kNeeBeta * N + slot], nee[(kNeeBeta + 1) * N + slot], nee[(kNeeBeta + 2) * N + slot]);
-    in.lpdf = nee[kNeeLpdf * N + slot];
-    if (portalA || (mis && (fl & kNfC1) && hA == 0))
-        in.F = s3(nee[kNeeF * N + slot], nee[(kNeeF + 1) * N + slot], nee[(kNeeF + 2) * N + slot]);
-    if ((portalA && hA < 0) || misB)
-        in.Li = s3(nee[kNeeLi * N + slot], nee[(kNeeLi + 1) * N + slot], nee[(kNeeLi + 2) * N + slot]);
-    if (portalA) in.pdf = nee[kNeePdf * N + slot];
-    if ((fl & kNfPortal) && (fl & kNfDivPortal)) in.w = nee[kNeePortalPdf * N + slot];
-    if (portalA && hA >= 0) in.ray = load_ray(ps.rayA, slot, kInf);
-    if (misB) {
-        in.nl = __float_as_int(nee[kNeeLight * N + slot]);
-        in.w = nee[kNeeSw * N + slot];
-        in.pdf = nee[kNeeSpdf * N + slot];
-        in.ray = load_ray(ps.rayB, slot, kInf);
+    const bool misB = kMis && !(fl & kNfPortal) && (fl & kNfMis) && (fl & kNfB);
+    const bool mis = kMis && !(fl & kNfPortal) && (fl & kNfMis);
+    const float4 q0 = q[0];  // beta, light-selection pdf
+    in.beta = s3(q0.x, q0.y, q0.z);
+    in.lpdf = q0.w;
+    if (portalA || (mis && (fl & kNfC1) && hA == 0)) {  // F, the portal estimators' pdf
+        const float4 q1 = q[1];
+        in.F = s3(q1.x, q1.y, q1.z);
+        if (portalA) in.pdf = q1.w;
     }
+    if ((portalA && hA < 0) || misB) {  // Li / f2, the MIS scattering weight
+        const float4 q2 = q[2];
+        in.Li = s3(q2.x, q2.y, q2.z);
+        if (misB) in.w = q2.w;
+    }
+    if (misB) {  // scattering pdf, MIS light
+        const float4 q3 = q[3];
+        in.pdf = q3.x;
+        in.nl = __float_as_int(q3.z);
+    } else if ((fl & kNfPortal) && (fl & kNfDivPortal)) {  // the projection estimator's portal pdf
+        in.w = q[3].y;
+    }
+    if (portalA && hA >= 0) in.ray = load_ray(ps.rayA, slot, kInf);
+    if (misB) in.ray = load_ray(ps.rayB, slot, kInf);
     return in;
 }
 // fl / hA / hB: the payload's flags and the hits of rays A and B.
@@ -1112,11 +1120,12 @@ __device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, 
     }
     return Ld;
 }
+// st: the path's state word (the payload's flags at kStNfShift)
 template <int kFt>
-__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot) {
-    const uint32_t fl = __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]);
-    const int hA = ps.hitA[slot];
-    return nee_value<kFt>(sc, ps, slot, fl, hA, ps.hitB[slot], nee_load(ps, slot, fl, hA));
+__device__ __forceinline__ S3 nee_value(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t st) {
+    const uint32_t fl = (st & kStNfMask) >> kStNfShift;
+    const int hA = *hit_word(ps, slot, kHdHitA);
+    return nee_value<kFt>(sc, ps, slot, fl, hA, *hit_word(ps, slot, kHdHitB), nee_load<Ft<kFt>::mis>(ps, slot, fl, hA));
 }
 template <int kFt>
 __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, uint32_t fl,
@@ -1126,7 +1135,7 @@ __device__ __forceinline__ void resolve_nee(const DevScene& sc, const DevPaths& 
 }
 
 __device__ __forceinline__ void put_nee(const DevPaths& ps, uint32_t slot, int k, float v) {
-    ps.nee[(uint32_t)k * (uint32_t)ps.n + slot] = v;
+    ps.nee[(uint32_t)kNee * slot + (uint32_t)k] = v;
 }
 __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int k, S3 v) {
     put_nee(ps, slot, k, v.c[0]); put_nee(ps, slot, k + 1, v.c[1]); put_nee(ps, slot, k + 2, v.c[2]);
@@ -1134,9 +1143,10 @@ __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int 
 
 // PortalArealight::EstimateDirect set-up (portal_arealight.cpp:29-239).
 // u1 = uScattering (argument order at integrator.cpp:132); u2 is unused; the
-// selected portal is call-local.  Returns true when ray A was emitted.
+// selected portal is call-local.  Returns the payload's kNf* flags (kNfA: ray
+// A was emitted); the caller keeps them in the path's state word.
 template <int kFt>
-__device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
+__device__ __forceinline__ uint32_t portal_nee(const DevScene& sc, const DevPaths& ps, uint32_t slot, int lightIdx,
                                            const SurfHit& it, const Bsdf& bsdf, float u10, float u11,
                                            uint32_t* ab = nullptr) {
     const DevLight& l = sc.lights[PT_IDX(lightIdx, sc.n_lights)];
@@ -1149,7 +1159,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
         // so dist[i] is 1 for portals in front of the point and 0 otherwise; the
         // CDF entries are recomputed with the same sequential float sums.
         const int np = l.n_portals;
-        if (np > 0 && PT_IDX(l.first_portal + np - 1, sc.n_pplanes) != l.first_portal + np - 1) return false;
+        if (np > 0 && PT_IDX(l.first_portal + np - 1, sc.n_pplanes) != l.first_portal + np - 1) return 0u;
         const DevPlane* portals = sc.portal_planes + l.first_portal;
         int nvis = 0;
         for (int i = 0; i < np; ++i) nvis += plane_in_front(portals[i], pObj) ? 1 : 0;
@@ -1219,9 +1229,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
                     flags |= kNfA;
                     if (ab) *ab += 24 + 12 + 4 + 12;
                 }
-                put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
-                if (ab) *ab += 4;
-                return (flags & kNfA) != 0;
+                return flags;
             }
         }
     }
@@ -1238,9 +1246,7 @@ __device__ __forceinline__ bool portal_nee(const DevScene& sc, const DevPaths& p
         flags |= kNfA;
         if (ab) *ab += 24 + 12 + 4 + 12;
     }
-    put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
-    if (ab) *ab += 4;
-    return (flags & kNfA) != 0;
+    return flags;
 }
 
 // EstimateDirect, MIS branch (integrator.cpp:137-258) for a DiffuseAreaLight.
@@ -1294,8 +1300,6 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
             }
         }
     }
-    put_nee(ps, slot, kNeeFlags, __uint_as_float(flags));
-    if (ab) *ab += 4;
     return flags;
 }
 
@@ -1307,7 +1311,6 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
 struct PathPre {
     uint32_t st, hidx;
     int hit, hitA, hitB;
-    uint32_t nfl;
     S3 L, beta;
     Ray ray;
     float eta;    // etaScale (Russian roulette reads it)
@@ -1321,30 +1324,39 @@ struct PathNow {
     NeeIn nee;
     PrimRec rec;
 };
-template <bool kTab>
+template <int kFt>
 __device__ __forceinline__ void path_load_now(const DevScene& sc, const DevPaths& ps, uint32_t slot, const PathPre& p,
                                               PathNow* q) {
-    if (p.st & kStNee) q->nee = nee_load(ps, slot, p.nfl, p.hitA);
+    if (p.st & kStNee) q->nee = nee_load<Ft<kFt>::mis>(ps, slot, (p.st & kStNfMask) >> kStNfShift, p.hitA);
     if ((p.st & kStCont) && p.hit >= 0) q->rec = prim_rec(sc, p.hit);
 }
-// Two stages: the head (state word, payload flags, hits) two paths ahead, the
-// body one path ahead and only what the head says this step will read.
+// Two stages: the head record (state word with the payload flags, hits) two
+// paths ahead, the body one path ahead and only what the head says this step
+// will read.
 __device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t slot, PathPre* p) {
-    p->st = ps.st[slot];
-    p->hit = ps.hit[slot];
-    p->hitA = ps.hitA[slot];
-    p->hitB = ps.hitB[slot];
-    p->nfl = __float_as_uint(ps.nee[kNeeFlags * (uint32_t)ps.n + slot]);
+    // four 4-B loads from the one 16-B record (a uint4 load pins four aligned registers two paths ahead)
+    p->st = *st_word(ps, slot);
+    p->hit = *hit_word(ps, slot, kHdHit);
+    p->hitA = *hit_word(ps, slot, kHdHitA);
+    p->hitB = *hit_word(ps, slot, kHdHitB);
 }
 __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t slot, PathPre* p) {
-    const uint32_t N = (uint32_t)ps.n;
-    p->L = load_s3(ps.L, N, slot);
+    const float3 a = *reinterpret_cast<const float3*>(body_word(ps, slot, kBdL));
+    p->L = s3(a.x, a.y, a.z);
     if (p->st & kStCont) {
-        p->hidx = ps.hidx[slot];
-        p->beta = load_s3(ps.beta, N, slot);
+        p->hidx = hidx_of(ps, slot);
+        const float4 b = ps.body[2u * slot + 1u];
+        p->beta = s3(b.x, b.y, b.z);
+        p->eta = b.w;
         p->ray = load_ray(ps.ray, slot, kInf);
-        p->eta = ps.eta[slot];
     }
+}
+__device__ __forceinline__ void store_L(const DevPaths& ps, uint32_t slot, S3 L) {
+    *reinterpret_cast<float3*>(body_word(ps, slot, kBdL)) = make_float3(L.c[0], L.c[1], L.c[2]);
+}
+__device__ __forceinline__ S3 load_L(const DevPaths& ps, uint32_t slot) {
+    const float4 a = ps.body[2u * slot];
+    return s3(a.x, a.y, a.z);
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
@@ -1354,14 +1366,13 @@ template <int kFt>
 __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl, const DevPaths& ps, uint32_t slot,
                                            const PathPre& pre, const PathNow& now, RayList* rays,
                                            bool* keep, bool* overflow, uint32_t* ab) {
-    const uint32_t N = (uint32_t)ps.n;
     rays->n = 0;
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
     uint32_t st = pre.st;
     S3 L = pre.L;
     *ab += 4 + 4 + 12 + 12 + 4;  // queue entry, st + L read, L + st written
     if (st & kStNee) {
-        const uint32_t fl = pre.nfl;
+        const uint32_t fl = (st & kStNfMask) >> kStNfShift;
         {   // bytes of the NEE payload resolve_nee reads (integrator.cpp:121, portal_arealight.cpp:29-239)
             uint32_t b = 4 + 12 + 4;  // flags, beta, light-selection pdf
             if (fl & kNfPortal) {
@@ -1374,7 +1385,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
             *ab += b;
         }
         resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.hitB, now.nee, &L);
-        st &= ~kStNee;
+        st &= ~(kStNee | kStNfMask);
     }
     if (st & kStCont) {
         st &= ~kStCont;
@@ -1413,6 +1424,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                 if (bsdf_num<kFt>(bsdf, kBxNonSpecular) > 0) {
                     // UniformSampleOneLight (integrator.cpp:100-122)
                     bool deferred = false;
+                    uint32_t nf = 0;  // the payload's kNf* flags
                     float lightPdf = 0;
                     bool haveLight = false;
                     if (sc.n_lights > 0) {
@@ -1424,15 +1436,16 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                             const float uL0 = dm.get1(), uL1 = dm.get1();
                             const float uS0 = dm.get1(), uS1 = dm.get1();
                             if (!Ft<kFt>::mis || sc.lights[PT_IDX(ln, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
-                                if (portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1, ab)) {
+                                nf = portal_nee<kFt>(sc, ps, slot, ln, si, bsdf, uS0, uS1, ab);
+                                if (nf & kNfA) {
                                     rays->push(slot << 2 | kRayA);
                                     deferred = true;
                                 }
                             } else {
-                                const uint32_t f = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1, ab);
-                                if (f & kNfA) rays->push(slot << 2 | kRayShadow);
-                                if (f & kNfB) rays->push(slot << 2 | kRayB);
-                                deferred = (f & (kNfA | kNfB)) != 0;
+                                nf = mis_nee<kFt>(sc, ps, slot, ln, si, bsdf, uL0, uL1, uS0, uS1, ab);
+                                if (nf & kNfA) rays->push(slot << 2 | kRayShadow);
+                                if (nf & kNfB) rays->push(slot << 2 | kRayB);
+                                deferred = (nf & (kNfA | kNfB)) != 0;
                             }
                         }
                     }
@@ -1440,7 +1453,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                         put_nee3(ps, slot, kNeeBeta, beta);
                         put_nee(ps, slot, kNeeLpdf, lightPdf);
                         *ab += 12 + 4;
-                        st |= kStNee;
+                        st = (st & ~kStNfMask) | kStNee | (nf << kStNfShift);
                     } else {
                         // no ray: EstimateDirect returned Spectrum(0)
                         L = L + beta * (haveLight ? s3(0.f) / lightPdf : s3(0.f));
@@ -1460,7 +1473,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     if (Ft<kFt>::spec && (sampled & kBxSpecular) && (sampled & kBxT)) {  // etaScale (path.cpp:144-150)
                         const float eta = bsdf.eta;
                         etaScale *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
-                        ps.eta[slot] = etaScale;
+                        *body_word(ps, slot, kBdEta) = etaScale;
                         *ab += 4;
                     }
                     *ab += 4;  // etaScale read for Russian roulette
@@ -1475,7 +1488,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     }
                     if (alive) {
                         store_ray(ps.ray, slot, r);
-                        store_s3(ps.beta, N, slot, beta);
+                        *reinterpret_cast<float3*>(body_word(ps, slot, kBdBeta)) = make_float3(beta.c[0], beta.c[1], beta.c[2]);
                         *ab += 24 + 12;
                         ++bounces;
                         st |= kStCont;
@@ -1483,13 +1496,13 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     }
                 }
                 if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
-                st = (st & ~kStDimMask) | ((uint32_t)dm.dim & kStDimMask);
+                st = (st & ~kStDimMask) | (uint32_t)min(dm.dim, (int)kStDimMask);  // past max_dim only after overflow
                 st = (st & ~(0xffu << kStBounceShift)) | ((uint32_t)(bounces & 0xff) << kStBounceShift);
             }
         }
     }
-    store_s3(ps.L, N, slot, L);
-    ps.st[slot] = st;
+    store_L(ps, slot, L);
+    *st_word(ps, slot) = st;
     *keep = (st & (kStCont | kStNee)) != 0;
     *ab += 4 * (rays->n + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
@@ -1561,7 +1574,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             PathNow now{};
             path_prefetch_head(ps, slot, &pre);
             path_prefetch_body(ps, slot, &pre);
-            path_load_now<kTab>(sc, ps, slot, pre, &now);
+            path_load_now<kFt>(sc, ps, slot, pre, &now);
             shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
         }
         wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
@@ -1583,7 +1596,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             uint32_t slot2 = 0;
             if (i < n) {
                 path_prefetch_body(ps, slot, &pre);
-                path_load_now<kTab>(sc, ps, slot, pre, &now);
+                path_load_now<kFt>(sc, ps, slot, pre, &now);
             }
             if (i + stride < n) path_prefetch_head(ps, slot1, &nxt);
             if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
@@ -1614,7 +1627,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         PathPre nn{};
         PathNow now{};
         uint32_t slot3 = 0;
-        if (i < n) path_load_now<kTab>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
+        if (i < n) path_load_now<kFt>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
         if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
         if (i + 2 * stride < n) path_prefetch_head(ps, slot2, &nn);
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
@@ -1663,15 +1676,15 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
     auto fl3 = [&](int k) { return s3(Fl[k * N + slot], Fl[(k + 1) * N + slot], Fl[(k + 2) * N + slot]); };
     auto setf3 = [&](int k, S3 v) { Fl[k * N + slot] = v.c[0]; Fl[(k + 1) * N + slot] = v.c[1]; Fl[(k + 2) * N + slot] = v.c[2]; };
 
-    uint32_t st = ps.st[slot];
+    uint32_t st = *st_word(ps, slot);
     rays->n = 0;
     int d = I[kDlD * N + slot];
-    Dims dm{&sc, ps.hidx[slot], (int)(st & kStDimMask), false};
+    Dims dm{&sc, hidx_of(ps, slot), (int)(st & kStDimMask), false};
     int step;
     S3 e = s3(0.f), Lc = s3(0.f);
     if (st & kStNee) {
-        e = nee_value<kFt>(sc, ps, slot);
-        st &= ~kStNee;
+        e = nee_value<kFt>(sc, ps, slot, st);
+        st &= ~(kStNee | kStNfMask);
         step = kDlAcc;
     } else {
         st &= ~kStCont;
@@ -1697,17 +1710,19 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
     // one EstimateDirect: emits its rays, or yields Ld = 0 at once
     auto estimate = [&](int j, float uL0, float uL1, float uS0, float uS1) -> bool {
         vertex();
+        uint32_t f;
         if (sc.lights[PT_IDX(j, sc.n_lights)].kind == PT_LIGHT_PORTAL_AREA) {
-            if (portal_nee<kFt>(sc, ps, slot, j, si, bsdf, uS0, uS1)) {
-                rays->push(slot << 2 | kRayA);
-                return true;
-            }
-            return false;
+            f = portal_nee<kFt>(sc, ps, slot, j, si, bsdf, uS0, uS1);
+            if (f & kNfA) rays->push(slot << 2 | kRayA);
+            f &= (f & kNfA) ? ~0u : 0u;
+        } else {
+            f = mis_nee<kFt>(sc, ps, slot, j, si, bsdf, uL0, uL1, uS0, uS1);
+            if (f & kNfA) rays->push(slot << 2 | kRayShadow);
+            if (f & kNfB) rays->push(slot << 2 | kRayB);
+            f &= (f & (kNfA | kNfB)) ? ~0u : 0u;
         }
-        const uint32_t f = mis_nee<kFt>(sc, ps, slot, j, si, bsdf, uL0, uL1, uS0, uS1);
-        if (f & kNfA) rays->push(slot << 2 | kRayShadow);
-        if (f & kNfB) rays->push(slot << 2 | kRayB);
-        return (f & (kNfA | kNfB)) != 0;
+        st = (st & ~kStNfMask) | (f << kStNfShift);  // the payload's flags ride in the state word
+        return f != 0;
     };
     // Sampler::Get2DArray entry k of array ai: GetIndexForSample(s * n + k) (sampler.cpp:149-160)
     auto array_u = [&](int ai, int k, int n, float* u0, float* u1) {
@@ -1733,7 +1748,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
         switch (step) {
             case kDlHit: {
                 const Ray ray = load_ray(ps.ray, slot, kInf);
-                const int hp = ps.hit[slot];
+                const int hp = *hit_word(ps, slot, kHdHit);
                 SurfHit h;
                 const bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, ray, &h);
                 if (!found) {  // Light::Le of every light: only infinite lights emit
@@ -1869,7 +1884,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
             }
             case kDlReturn: {
                 if (d == 0) {
-                    store_s3(ps.L, N, slot, Lc);
+                    store_L(ps, slot, Lc);
                     step = kDlDone;
                     break;
                 }
@@ -1885,8 +1900,8 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
     }
     I[kDlD * N + slot] = d;
     if (dm.overflow) { st |= kStDimOverflow; *overflow = true; }
-    st = (st & ~kStDimMask) | ((uint32_t)dm.dim & kStDimMask);
-    ps.st[slot] = st;
+    st = (st & ~kStDimMask) | (uint32_t)min(dm.dim, (int)kStDimMask);  // past max_dim only after overflow
+    *st_word(ps, slot) = st;
     *keep = (st & (kStCont | kStNee)) != 0;
 }
 
@@ -1983,7 +1998,6 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
                                               int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum)
 #ifdef PT_TU_MISC
 {
-    const uint32_t N = (uint32_t)ps.n;
     const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
     const int total = bw * bh;
@@ -2022,7 +2036,7 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
                                 const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
                                 touch = !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
                                 if (touch) {
-                                    S3 L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                                    S3 L = load_L(ps, slot);
                                     if (has_nan(L)) L = s3(0.f);
                                     else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
                                     else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
@@ -2084,7 +2098,6 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
     __shared__ float s_tab[256];
     if (threadIdx.x < 256) s_tab[threadIdx.x] = fc.table[threadIdx.x];
     __syncthreads();
-    const uint32_t N = (uint32_t)ps.n;
     const int cw = fc.crop_x1 - fc.crop_x0;
     const int sbw = fc.sb_x1 - fc.sb_x0;
     const int lane = (int)lane_id();
@@ -2128,7 +2141,7 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
                                 y0 = (int)ceilf(dy - fc.ry); y1 = (int)floorf(dy + fc.ry) + 1;
                                 reach = !(gx1 < x0 || gx0 >= x1 || gy1 < y0 || gy0 >= y1);
                                 if (reach) {
-                                    L = s3(ps.L[slot], ps.L[N + slot], ps.L[2 * N + slot]);
+                                    L = load_L(ps, slot);
                                     if (has_nan(L)) L = s3(0.f);
                                     else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
                                     else if (__builtin_isinf(lum_y(L))) L = s3(0.f);

@@ -164,10 +164,12 @@ struct Frame {
 constexpr int kMaxPipes = 4;  // render_tiles pipelines (PT_PIPES)
 
 struct Work {
-    DBuf<uint32_t> hidx, st, rq0, rq1, pq0, pq1, counts;
+    DBuf<uint32_t> rq0, rq1, pq0, pq1, counts;
+    DBuf<uint4> head;   // DevPaths records (device.h)
+    DBuf<float4> body;
     DBuf<float2> pfilm;
-    DBuf<float> L, beta, eta, ray, rayA, rayB, nee;
-    DBuf<int> hit, hitA, hitB, spill;
+    DBuf<float> ray, rayA, rayB, nee;
+    DBuf<int> spill;
     DBuf<DevStats> stats;
     DBuf<int> dli;                 // DirectLighting state (kDl*)
     DBuf<float> dlf, dlframe;
@@ -207,9 +209,9 @@ struct Work {
             dl_frames = frames;
         }
         if (n > cap) {
-            hidx.alloc(n); st.alloc(n); rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
-            pfilm.alloc(n); L.alloc(3 * n); beta.alloc(3 * n); eta.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
-            rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); hit.alloc(n); hitA.alloc(n); hitB.alloc(n);
+            rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
+            head.alloc(n); body.alloc(2 * n); pfilm.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
+            rayB.alloc(8 * n); nee.alloc((size_t)kNee * n);
             cap = n;
         }
         spill.alloc(spill_threads * 64);  // k_trace_pt: 64 words per lane (entries past its LDS rows)
@@ -219,8 +221,8 @@ struct Work {
     DevPaths paths(int n) {
         DevPaths p{};
         p.n = n;
-        p.hidx = hidx.p; p.pfilm = pfilm.p; p.L = L.p; p.beta = beta.p; p.eta = eta.p; p.st = st.p;
-        p.ray = ray.p; p.hit = hit.p; p.rayA = rayA.p; p.hitA = hitA.p; p.rayB = rayB.p; p.hitB = hitB.p;
+        p.head = head.p; p.body = body.p; p.pfilm = pfilm.p;
+        p.ray = ray.p; p.rayA = rayA.p; p.rayB = rayB.p;
         p.nee = nee.p;
         p.dli = dl_frames > 0 ? dli.p : nullptr;
         p.dlf = dl_frames > 0 ? dlf.p : nullptr;
@@ -2124,7 +2126,9 @@ pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, 
         launch_trace(s, w, ps, w.rq0.p, w.counts.p, (uint32_t)n, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipDeviceSynchronize());
-        HIPCHK(hipMemcpy(out_prim, any ? w.hitA.p : w.hit.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+        // hit words of the head records (device.h): hit for closest-hit queries, hitA for any-hit ones
+        HIPCHK(hipMemcpy2D(out_prim, sizeof(int32_t), (const int*)w.head.p + (any ? kHdHitA : kHdHit), sizeof(uint4),
+                           sizeof(int32_t), (size_t)n, hipMemcpyDeviceToHost));
         if (counters) {
             DevStats d;
             HIPCHK(hipMemcpy(&d, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));

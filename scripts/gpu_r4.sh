@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 evidence on one GPU.  Every GPU step has its own time limit; the
 # script stops at the first failure.
-#   STAGES (default "tests bench prof pmc sq"): any subset, in this order
+#   STAGES (default "tests bench prof pmc sq"): any subset of tests bench ab prof pmc sq, run in that order
 #   CFG    bench --config for bench/prof/pmc/sq (default c2); OUT tag (default $CFG)
 #   BARGS  extra bench args for prof/pmc (e.g. "--spp 64")
 # Outputs under gpurun_out/r4_$OUT/: source_hash.txt, pytest_gpu.log, smoke.log,
@@ -29,6 +29,18 @@ if has bench; then
   timeout -k 10 600 python -u bench.py --config "$CFG" --steps ${STEPS:-10} --warmup ${WARMUP:-2} --cpu-seconds 15 \
     ${EMUL:+--emulate-ranks $EMUL} $BARGS > "$o/bench.log" 2>&1
   rc=$?; echo "bench rc=$rc"; tail -1 "$o/bench.log" | cut -c1-600; ok $rc bench
+fi
+if has ab; then
+  # A/B: one short bench per environment in ABENVS ("A=1 B=2;C=3;" -- ';'-separated, empty = default)
+  IFS=';' read -ra envs <<< "${ABENVS:-}"
+  i=0
+  for e in "${envs[@]}"; do
+    i=$((i+1))
+    env $e timeout -k 10 300 python -u bench.py --config "$CFG" --steps ${ABSTEPS:-5} --warmup 1 --no-cpu-baseline $BARGS \
+      > "$o/ab_$i.log" 2>&1
+    rc=$?; echo "ab $i [$e] rc=$rc $(tail -1 "$o/ab_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); k=d["roofline_kernels"]; print(d["value"], d["ms_per_step"], {x: (v["kernel"], v["avg_launch_ms"], v["isolated_avg_launch_ms"]) for x, v in k.items()})' 2>/dev/null)"
+    ok $rc "ab $i"
+  done
 fi
 cd /tmp || exit 1
 if has prof; then

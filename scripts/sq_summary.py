@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the SQ counter passes of scripts/gpu_pmc_sq.sh into
+"""Summarise the SQ counter passes of scripts/gpu_r4.sh (stage sq) into
 profiles/<round>_sq_counters.json: per kernel, the counters summed over its
 dispatches and the ratios the DESIGN quotes (share of wave cycles spent
 waiting, instructions per wave by kind).
@@ -42,7 +42,7 @@ if not src:
     import bench
     src = bench.source_hash()
 out = {"workload": a.workload, "config": a.config, "source_hash": src, "bench_args": a.args,
-       "method": "rocprofv3 --pmc, two passes of 8 SQ counters each (scripts/gpu_pmc_sq.sh); sums over dispatches",
+       "method": "rocprofv3 --pmc, two passes of 8 SQ counters each (scripts/gpu_r4.sh (stage sq)); sums over dispatches",
        "kernels": {}}
 for k, c in sums.items():
     w = c.get("SQ_WAVES", 0) or 1
