@@ -227,16 +227,20 @@ def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: boo
       LDS table, ~150 TB/s), with the SQ issue view beside it.
     * shading: the path-state bytes each path step must read and write (the
       state PathIntegrator::Li carries between vertices + queue entries),
-      counted on the device per step (kernels.hip shade_path)."""
+      counted on the device per step (kernels.hip shade_path) in the extra
+      frame (pt_set_count_bytes)."""
     trace_name, shade_name = names
     ks = {}
-    parts = [("k_trace", trace_name, "trace", 32.0 * timed["node_visits"] + 48.0 * timed["prim_tests"])]
-    if timed["shade_bytes"] > 0:
-        parts.append(("k_shade", shade_name, "shade", float(timed["shade_bytes"])))
-    for key, kname, p, alg_total in parts:
+    # algorithmic bytes per launch: the trace counters of the timed steps; the shading kernel's count from the
+    # extra frame (counted by the pt_set_count_bytes build; the same batches, bounces and launches)
+    parts = [("k_trace", trace_name, "trace", (32.0 * timed["node_visits"] + 48.0 * timed["prim_tests"]) /
+              max(1, timed["trace_launches"]))]
+    if iso["shade_bytes"] > 0:
+        parts.append(("k_shade", shade_name, "shade",
+                      float(iso["shade_bytes"]) / max(1, iso.get("shade_launches_counted", iso["shade_launches"]))))
+    for key, kname, p, alg in parts:
         nl = max(1, timed[p + "_launches"])
         avg = timed[p + "_ms"] / nl
-        alg = alg_total / nl
         il = max(1, iso[p + "_launches"])
         trf, trf_src, stale = pmc_traffic(workload, kname, src)
         e = {"kernel": kname, "launches": timed[p + "_launches"], "avg_launch_ms": round(avg, 4),
@@ -408,6 +412,14 @@ def main():
     sc.set_pipelines(pipes)
     for k in iso:
         iso[k] = st[k]
+    # and one frame with the shading build that also counts its algorithmic path-state bytes (one more
+    # register: a separate instantiation, pt_set_count_bytes; the same batches, bounces and launches)
+    sc.set_count_bytes(True)
+    accum.zero_()
+    st = render(my)
+    torch.cuda.synchronize()
+    sc.set_count_bytes(False)
+    iso["shade_bytes"], iso["shade_launches_counted"] = st["shade_bytes"], st["shade_launches"]
     emul = None
     if args.emulate_ranks and world == 1:
         # every rank's tile shard at N ranks, one after the other, each timed like a step

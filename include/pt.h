@@ -287,7 +287,8 @@ typedef struct pt_stats {
     uint64_t trace_launches;
     double shade_ms;           /* summed duration of the shading kernel */
     uint64_t shade_launches;
-    uint64_t shade_bytes;      /* path integrator: algorithmic path-state bytes the shading kernel moved */
+    uint64_t shade_bytes;      /* path integrator: algorithmic path-state bytes the shading kernel moved
+                                  (0 unless pt_set_count_bytes is on) */
     double reduce_ms;          /* pt_render_frame_dist: the ncclReduce of the film (HIP events on the stream) */
 } pt_stats;
 
@@ -404,6 +405,10 @@ pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
  * and its own path-state buffers; one batch's trace kernel overlaps another's
  * shading.  1 runs the batches one after the other (isolated kernel timings). */
 pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
+/* Count the shading kernel's algorithmic path-state bytes (pt_stats.shade_bytes)
+ * in the renders that follow (default off: the count costs the 3-waves-per-SIMD
+ * shading build a register, so it runs a separate instantiation). */
+pt_status pt_set_count_bytes(pt_scene* scene, int32_t on);
 
 /* Read back a setting of a device scene (what the environment overrides and
  * the pt_set_* calls left in effect), so callers can restore or report it.
@@ -415,7 +420,8 @@ enum pt_scene_key {
     PT_Q_TRACE_LDS_BYTES = 2,  /* bytes of BVH + primitives the trace kernel stages in LDS (0 = reads HBM) */
     PT_Q_TRACE_SPILL = 3,      /* 1 when traversal stacks spill past the LDS rows (deep BVHs) */
     PT_Q_FEATURES = 4,         /* scene-feature set the shading kernel is instantiated for */
-    PT_Q_TRACE_KERNEL = 5,     /* traversal kernel of a render: 0 k_trace, 1 k_trace_pt, 2 k_trace_nb, 3 k_trace_lds */
+    PT_Q_TRACE_KERNEL = 5,     /* traversal kernel of a render: 0 k_trace, 1 k_trace_pt, 2 k_trace_nb, 3 k_trace_lds,
+                                  4 k_trace_lds2 */
     PT_Q_SHADE_KERNEL = 6      /* shading kernel: 0 k_shade, 3 k_shade_w3, 5 k_shade_tab, 6 k_shade_dl,
                                   7 / 8 / 9 k_shade_hero / _w2 / _w4 */
 };

@@ -924,6 +924,233 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
 #endif
 
 // ----------------------------------------------------------------------------
+// k_trace_lds2: k_trace_lds with TWO rays per lane.  A node step of k_trace_lds
+// is one dependent chain (LDS node + stack top -> box test -> next address);
+// with one ray per lane only other waves hide its LDS and ALU latency.  Here
+// each lane carries ray slots 0 and 1, their node reads are issued together
+// under one wait, and both box tests run in one basic block (the step kind
+// and the per-slot `go` conditions are lane masks, not branches), so the two
+// chains interleave.  Each slot keeps its own LDS stack column (two stack
+// regions per block).  A slot's sequence of node visits, primitive tests and
+// tMax updates is k_trace_lds's, so hits and counters are the reference's.
+// ----------------------------------------------------------------------------
+struct Tr2 {
+    Ray ray;
+    V3 inv;
+    TriShear sh;
+    uint32_t sgn, sp, cur, slot, kind;
+    int hitPrim, leafPos, leafEnd;
+    bool active, n0, n1, n2;
+};
+__device__ __forceinline__ void tr2_start(Tr2& t, const DevScene& sc, const DevPaths& ps, uint32_t e, uint32_t node0,
+                                          uint32_t sbase, uint32_t* nrays) {
+    t.slot = e >> 2;
+    t.kind = e & 3u;
+    t.ray = load_ray_trace(t.kind == kRayCont ? ps.ray : (t.kind == kRayB ? ps.rayB : ps.rayA), t.slot,
+                           t.kind == kRayShadow);
+    t.inv = v3(1 / t.ray.d.x, 1 / t.ray.d.y, 1 / t.ray.d.z);
+    t.sh = tri_shear(t.ray.d);
+    t.n0 = t.inv.x < 0; t.n1 = t.inv.y < 0; t.n2 = t.inv.z < 0;
+    t.sgn = (t.n0 ? 1u << 16 : 0u) | (t.n1 ? 1u << 17 : 0u) | (t.n2 ? 1u << 18 : 0u);
+    t.cur = node0; t.sp = sbase; t.hitPrim = -1; t.leafPos = 0; t.leafEnd = 0;
+    t.active = sc.n_nodes > 0;  // empty scene: every ray misses
+    if (!t.active) {
+        if (t.kind == kRayShadow) *hit_word(ps, t.slot, kHdHitA) = 0;
+        else if (t.kind == kRayCont) *hit_word(ps, t.slot, kHdHit) = -1;
+        else if (t.kind == kRayA) *hit_word(ps, t.slot, kHdHitA) = -1;
+        else *hit_word(ps, t.slot, kHdHitB) = -1;
+    }
+    *nrays += t.kind == kRayShadow ? 0x10000u : 1u;
+}
+__device__ __forceinline__ void tr2_finish(Tr2& t, const DevPaths& ps) {
+    if (t.kind == kRayShadow) *hit_word(ps, t.slot, kHdHitA) = t.hitPrim >= 0 ? 1 : 0;
+    else if (t.kind == kRayCont) *hit_word(ps, t.slot, kHdHit) = t.hitPrim;
+    else if (t.kind == kRayA) *hit_word(ps, t.slot, kHdHitA) = t.hitPrim;
+    else *hit_word(ps, t.slot, kHdHitB) = t.hitPrim;
+    t.active = false;
+}
+// up to kLeafSteps primitive tests of slot t's leaf; returns true when the ray is finished
+template <bool kSph>
+__device__ __forceinline__ bool tr2_leaf(Tr2& t, const DevScene& sc, const float4* bprims, uint32_t sbase,
+                                         uint32_t* prims) {
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u < kLeafSteps; ++u) {
+        if (!(!done && t.leafPos < t.leafEnd)) continue;
+        const int pi = t.leafPos++;
+        ++*prims;
+        const float4 r0 = bprims[3 * pi];
+        const float4 r1 = bprims[3 * pi + 1];
+        const float4 r2 = bprims[3 * pi + 2];
+        const uint32_t fl = __float_as_uint(r0.w);
+        float tt = 0;
+        bool ok;
+        if (fl & kPrimAnalytic) {
+            ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), t.ray, &tt);
+        } else {
+            ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), t.ray, t.sh, &tt);
+            ok &= (t.kind == kRayShadow) | !(fl & kPrimDegenerate);
+        }
+        t.hitPrim = ok ? pi : t.hitPrim;
+        t.ray.tmax = (ok && t.kind != kRayShadow) ? tt : t.ray.tmax;
+        done = ok && t.kind == kRayShadow;
+        if (!done && t.leafPos == t.leafEnd) {  // the leaf is finished: pop
+            const bool empty = t.sp == sbase;
+            done = empty;
+            if (!empty) {
+                t.cur = (uint32_t)lds_top(t.sp);
+                t.sp -= 512;
+            }
+        }
+    }
+    return done;
+}
+// the two slots' nodes and stack tops, one wait
+__device__ __forceinline__ void lds_node_top2(uint32_t addr0, uint32_t sp0, uint32_t addr1, uint32_t sp1, float4* a0,
+                                              float4* b0, int* top0, float4* a1, float4* b1, int* top1) {
+    float4 x0, y0, x1, y1;
+    int t0, t1;
+    asm volatile(
+        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %6 offset:16\n\tds_read_b32 %2, %7\n\t"
+        "ds_read_b128 %3, %8\n\tds_read_b128 %4, %8 offset:16\n\tds_read_b32 %5, %9\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(y0), "=&v"(t0), "=&v"(x1), "=&v"(y1), "=&v"(t1)
+        : "v"(addr0), "v"(sp0), "v"(addr1), "v"(sp1)
+        : "memory");
+    *a0 = x0; *b0 = y0; *top0 = t0;
+    *a1 = x1; *b1 = y1; *top1 = t1;
+}
+// one node visit of slot t when go (lane mask), k_trace_lds's step with every
+// state update predicated on go; returns whether the ray finished
+__device__ __forceinline__ bool tr2_node(Tr2& t, bool go, float4 a, float4 b, int top, uint32_t sbase,
+                                         uint32_t* nodes) {
+    *nodes += go ? 1u : 0u;
+    const bool hit = box_hit_mm(a, b, t.ray, t.inv, t.n0, t.n1, t.n2);
+    const uint32_t off = __float_as_uint(b.z);  // leaf: primitivesOffset; interior: second child
+    const uint32_t w = __float_as_uint(b.w);
+    const bool inner = go & hit & ((int)w < 0);
+    const bool leaf = go & hit & ((int)w >= 0);
+    const bool neg = (w & t.sgn) != 0;
+    const bool empty = t.sp == sbase;
+    // the far child, written above the top whether or not it is kept (kept only for an interior node of a
+    // going slot; otherwise the row above the top is free)
+    lds_push(t.sp, (int)(neg ? t.cur + 32u : off));
+    const bool done = go & !hit & empty;
+    const bool pop = go & !hit & !empty;
+    t.cur = inner ? (neg ? off : t.cur + 32u) : (pop ? (uint32_t)top : t.cur);
+    t.sp = inner ? t.sp + 512 : (pop ? t.sp - 512 : t.sp);
+    t.leafPos = leaf ? (int)off : t.leafPos;
+    t.leafEnd = leaf ? (int)w : t.leafEnd;
+    return done;
+}
+
+// kW: waves per SIMD the register budget is set for (4: no spill; 5: a 20-B spill)
+template <bool kSph, int kW>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kSph ? 1 : kW))) void k_trace_lds2(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
+                                                            const uint32_t* __restrict__ rq_count, uint32_t* fetch,
+                                                            int refill_min, int leaf_min, int stack_rows,
+                                                            DevStats* stats)
+#ifdef PT_TU_TRACE
+{
+    extern __shared__ float4 lds_dyn[];
+    const int nn = 2 * sc.n_nodes;
+    const int scene_f4 = nn + 3 * sc.n_prims;
+    const uint32_t node0 = (uint32_t)(uintptr_t)lds_dyn;
+    for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
+        float4 v = i < nn ? sc.nodes[i] : sc.prims[i - nn];
+        if (i < nn && (i & 1)) {  // the node encoding of k_trace_lds
+            const uint32_t npax = __float_as_uint(v.w);
+            const uint32_t np = npax & 0xffffu;
+            const uint32_t off = (uint32_t)__float_as_int(v.z);
+            v.w = __uint_as_float(np ? off + np : 0x80000000u | (1u << (16 + (npax >> 16))));
+            if (!np) v.z = __uint_as_float(node0 + 32u * off);
+        }
+        lds_dyn[i] = v;
+    }
+    __syncthreads();
+    const float4* bprims = lds_dyn + nn;
+    // two stack regions of (stack_rows + 2) rows; the lane's column in each
+    const uint32_t srow = (uint32_t)(uintptr_t)((int*)(lds_dyn + scene_f4) + threadIdx.x);
+    const uint32_t sbase0 = srow, sbase1 = srow + (uint32_t)(stack_rows + 2) * 512u;
+    const uint32_t n = *rq_count;
+    const uint32_t lane = lane_id();
+    uint32_t nrays = 0, nodes = 0, prims = 0;
+    unsigned long long iters_w = 0;
+    bool exhausted = false, drained = false;
+    uint32_t qn = 0, qe = 0;
+    Tr2 t0, t1;
+    t0.ray = t1.ray = Ray{v3(0, 0, 0), v3(0, 0, 1), 0};
+    t0.inv = t1.inv = v3(0, 0, 0);
+    t0.sh = t1.sh = TriShear{0, 0, 0, 0};
+    t0.sgn = t1.sgn = 0;
+    t0.sp = sbase0; t1.sp = sbase1;
+    t0.cur = t1.cur = node0;
+    t0.slot = t1.slot = 0; t0.kind = t1.kind = 0;
+    t0.hitPrim = t1.hitPrim = -1;
+    t0.leafPos = t1.leafPos = t0.leafEnd = t1.leafEnd = 0;
+    t0.active = t1.active = false;
+    t0.n0 = t0.n1 = t0.n2 = t1.n0 = t1.n1 = t1.n2 = false;
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t idle0 = __ballot(!t0.active), idle1 = __ballot(!t1.active);
+            const uint32_t ni0 = (uint32_t)__popcll(idle0);
+            const uint32_t nidle = ni0 + (uint32_t)__popcll(idle1);
+            if (nidle >= (uint32_t)refill_min || nidle == 128u) {
+                if (qn >= qe && !drained) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
+                    base = (uint32_t)__shfl((int)base, 0);
+                    qn = base < n ? base : n;
+                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
+                    drained = base + kTraceChunk >= n;
+                }
+                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
+                const uint32_t k0 = lanes_below(idle0), k1 = ni0 + lanes_below(idle1);
+                const uint32_t i0 = qn + k0, i1 = qn + k1;
+                qn += take;
+                if (drained && qn >= qe) exhausted = true;
+                if (!t0.active && k0 < take) tr2_start(t0, sc, ps, rq[i0], node0, sbase0, &nrays);
+                if (!t1.active && k1 < take) tr2_start(t1, sc, ps, rq[i1], node0, sbase1, &nrays);
+            }
+        }
+        const bool wl0 = t0.active && t0.leafPos < t0.leafEnd, wl1 = t1.active && t1.leafPos < t1.leafEnd;
+        const bool wn0 = t0.active && !wl0, wn1 = t1.active && !wl1;
+        const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wl0)) + (uint32_t)__popcll(__ballot(wl1));
+        const uint32_t nNode = (uint32_t)__popcll(__ballot(wn0)) + (uint32_t)__popcll(__ballot(wn1));
+        if ((nLeaf | nNode) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        ++iters_w;
+        bool done0 = false, done1 = false;
+        if (leafStep) {
+            if (wl0) done0 = tr2_leaf<kSph>(t0, sc, bprims, sbase0, &prims);
+            if (wl1) done1 = tr2_leaf<kSph>(t1, sc, bprims, sbase1, &prims);
+        } else {
+            // kNodeSteps node visits per loop iteration for the slots in node mode
+#pragma unroll
+            for (int u = 0; u < kNodeSteps; ++u) {
+                const bool go0 = wn0 && !done0 && t0.leafPos >= t0.leafEnd;
+                const bool go1 = wn1 && !done1 && t1.leafPos >= t1.leafEnd;
+                if (!(go0 | go1)) continue;
+                float4 a0, b0, a1, b1;
+                int top0, top1;
+                lds_node_top2(t0.cur, t0.sp, t1.cur, t1.sp, &a0, &b0, &top0, &a1, &b1, &top1);
+                done0 |= tr2_node(t0, go0, a0, b0, top0, sbase0, &nodes);
+                done1 |= tr2_node(t1, go1, a1, b1, top1, sbase1, &nodes);
+            }
+        }
+        if (done0) tr2_finish(t0, ps);
+        if (done1) tr2_finish(t1, ps);
+    }
+    flush_stats(stats, nrays & 0xffffu, nrays >> 16, nodes, prims);
+    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 128ull * iters_w);
+}
+#else
+;
+#endif
+
+// ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
 // (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
 // ----------------------------------------------------------------------------
@@ -1370,7 +1597,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
     if (PT_IDX((int)slot, ps.n) != (int)slot) return;
     uint32_t st = pre.st;
     S3 L = pre.L;
-    *ab += 4 + 4 + 12 + 12 + 4;  // queue entry, st + L read, L + st written
+    if (ab) *ab += 4 + 4 + 12 + 12 + 4;  // queue entry, st + L read, L + st written
     if (st & kStNee) {
         const uint32_t fl = (st & kStNfMask) >> kStNfShift;
         {   // bytes of the NEE payload resolve_nee reads (integrator.cpp:121, portal_arealight.cpp:29-239)
@@ -1382,7 +1609,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                 if (fl & kNfC1) b += 4 + 12;
                 if (fl & kNfB) b += 4 + 4 + 12 + 4 + 4 + (pre.hitB >= 0 ? 24 : 0);
             }
-            *ab += b;
+            if (ab) *ab += b;
         }
         resolve_nee<kFt>(sc, ps, slot, fl, pre.hitA, pre.hitB, now.nee, &L);
         st &= ~(kStNee | kStNfMask);
@@ -1394,7 +1621,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
         const Ray ray = pre.ray;
         const int hp = pre.hit;
         S3 beta = pre.beta;
-        *ab += 24 + 4 + 12;
+        if (ab) *ab += 24 + 4 + 12;
         SurfHit si;
         bool found = hp >= 0 && surface_at<Ft<kFt>::sph>(sc, hp, now.rec, ray, &si);
         int mat = -1, light = -1;
@@ -1410,12 +1637,12 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                 // null BSDF: continue through the surface, bounces unchanged (path.cpp:108-113)
                 const Ray r{offset_ray_origin(si.p, si.perr, si.n, ray.d), ray.d, kInf};
                 store_ray(ps.ray, slot, r);
-                *ab += 24;
+                if (ab) *ab += 24;
                 st |= kStCont;
                 rays->push(slot << 2 | kRayCont);
             } else {
                 DimsL dm{&sc, &hl, pre.hidx, (int)(st & kStDimMask), false};
-                *ab += 4;
+                if (ab) *ab += 4;
                 Bsdf bsdf;
                 // Camera::GenerateWvls (camera.cpp:62-76): wvls[0] from camera dimension 5
                 const float wvl0 = Ft<kFt>::spec && sc.mats[PT_IDX(mat, sc.n_mats)].kind == PT_MAT_DISPERSIVE_GLASS
@@ -1452,7 +1679,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     if (deferred) {
                         put_nee3(ps, slot, kNeeBeta, beta);
                         put_nee(ps, slot, kNeeLpdf, lightPdf);
-                        *ab += 12 + 4;
+                        if (ab) *ab += 12 + 4;
                         st = (st & ~kStNfMask) | kStNee | (nf << kStNfShift);
                     } else {
                         // no ray: EstimateDirect returned Spectrum(0)
@@ -1474,9 +1701,9 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                         const float eta = bsdf.eta;
                         etaScale *= (dot(-ray.d, si.n) > 0) ? (eta * eta) : 1 / (eta * eta);
                         *body_word(ps, slot, kBdEta) = etaScale;
-                        *ab += 4;
+                        if (ab) *ab += 4;
                     }
-                    *ab += 4;  // etaScale read for Russian roulette
+                    if (ab) *ab += 4;  // etaScale read for Russian roulette
                     const Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf};
                     bool alive = true;
                     // Russian roulette (path.cpp:177-185)
@@ -1489,7 +1716,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                     if (alive) {
                         store_ray(ps.ray, slot, r);
                         *reinterpret_cast<float3*>(body_word(ps, slot, kBdBeta)) = make_float3(beta.c[0], beta.c[1], beta.c[2]);
-                        *ab += 24 + 12;
+                        if (ab) *ab += 24 + 12;
                         ++bounces;
                         st |= kStCont;
                         rays->push(slot << 2 | kRayCont);
@@ -1504,7 +1731,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
     store_L(ps, slot, L);
     *st_word(ps, slot) = st;
     *keep = (st & (kStCont | kStNee)) != 0;
-    *ab += 4 * (rays->n + (*keep ? 1u : 0u));  // ray / path queue entries written
+    if (ab) *ab += 4 * (rays->n + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
 
 // Copy n 4-byte words global -> LDS, the whole block.
@@ -1543,7 +1770,12 @@ __device__ __forceinline__ DevScene stage_tables(const DevScene& sc, uint4* lds)
 // kLean: the current path's body is loaded at the start of its own step
 // (ahead of the next path's head prefetch) instead of one path ahead -- the
 // register budget of 3 waves per SIMD for the kernels with the MIS branch.
-template <int kFt, bool kTab, bool kLean = false>
+// kAb: count the algorithmic path-state bytes (shade_path's ab) -- one
+// register, which the 3-wave build cannot spare, so the counting build is a
+// separate instantiation that the renderer runs only on request
+// (pt_set_count_bytes; the bench's one extra frame).
+#define PT_ABP (kAb ? &ab : nullptr)
+template <int kFt, bool kTab, bool kLean = false, bool kAb = false>
 __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
@@ -1575,7 +1807,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             path_prefetch_head(ps, slot, &pre);
             path_prefetch_body(ps, slot, &pre);
             path_load_now<kFt>(sc, ps, slot, pre, &now);
-            shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
+            shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, PT_ABP);
         }
         wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
     }
@@ -1602,7 +1834,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
             RayList rays;
             bool keep = false;
-            if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
+            if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, PT_ABP);
             wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
             slot = slot1;
             slot1 = slot2;
@@ -1633,7 +1865,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
         RayList rays;
         bool keep = false;
-        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, &ab);
+        if (i < n) shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, PT_ABP);
         wq_push(wq, rays, keep, slot, rq_out_count, rq_out, pq_out);
         slot = slot1;
         slot1 = slot2;
@@ -1645,8 +1877,10 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
 #endif
     wq_flush(wq, rq_out_count, rq_out, pq_out);
     if (overflow) atomicAdd(&stats->dim_overflow, 1ull);
-    const unsigned long long abw = wave_sum_u64((unsigned long long)ab);
-    if (lane_id() == 0 && abw) atomicAdd(&stats->shade_bytes, abw);
+    if (kAb) {
+        const unsigned long long abw = wave_sum_u64((unsigned long long)ab);
+        if (lane_id() == 0 && abw) atomicAdd(&stats->shade_bytes, abw);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1936,39 +2170,39 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_dl(DevScene sc, DevPaths 
 // Register-budget variants of the shading kernel (occupancy vs spills), each
 // compiled for a scene-feature set kFt; render.hip picks one (PT_SHADE_VARIANT,
 // scene_features).
-template <int kFt>
+template <int kFt, bool kAb>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
                                                        const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                                        uint32_t* rq_out_count, uint32_t* pq_out,
                                                        uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, false>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, false, false, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;
 #endif
 // The scene tables in LDS (stage_tables): scenes whose tables fit kTabLdsMax.
-template <int kFt>
+template <int kFt, bool kAb>
 __global__ __launch_bounds__(kShadeBlock) void k_shade_tab(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
                                                            const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                                            uint32_t* rq_out_count, uint32_t* pq_out,
                                                            uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, true>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, true, false, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;
 #endif
 // k_shade_tab with a 3-waves-per-SIMD register budget (PT_SHADE_VARIANT=3)
-template <int kFt>
+template <int kFt, bool kAb>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(
     DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
     uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, true, Ft<kFt>::mis>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, true, Ft<kFt>::mis, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;

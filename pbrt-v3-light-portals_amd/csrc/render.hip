@@ -278,12 +278,15 @@ struct pt_scene {
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
     bool shade_tab = false;      // k_shade_tab: the scene tables staged in LDS as well (small scenes)
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
+    bool count_bytes = false;    // pt_set_count_bytes: the shading build that counts algorithmic path-state bytes
     int shade_variant = 0;       // 0: compiler register budget, 3: k_shade_tab at 3 waves per SIMD (default when
                                  // that build has no scratch), 5: k_shade_tab
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
+    bool trace_2r = false;       // k_trace_lds2: two rays per lane (PT_TRACE_2R=1: 4 waves per SIMD, =2: 5)
+    int trace_2r_waves = 4;
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
@@ -347,23 +350,24 @@ static int scene_features(const pt_scene_desc* d) {
 using ShadeKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                              uint32_t*, DevStats*);
 template <int kFt>
-static ShadeKernel shade_kernel_ft(int variant) {
+static ShadeKernel shade_kernel_ft(int variant, bool ab) {
     switch (variant) {
-        case 3: return k_shade_w3<kFt>;
-        case 5: return k_shade_tab<kFt>;
-        default: return k_shade<kFt>;
+        case 3: return ab ? k_shade_w3<kFt, true> : k_shade_w3<kFt, false>;
+        case 5: return ab ? k_shade_tab<kFt, true> : k_shade_tab<kFt, false>;
+        default: return ab ? k_shade<kFt, true> : k_shade<kFt, false>;
     }
 }
 // Instantiated feature sets: all-matte, + infinite light, + spheres, + both,
 // everything.  Other combinations take the full kernel.
-static ShadeKernel shade_kernel(int variant, int features) {
-    if (features == kFtPortalOnly) return shade_kernel_ft<kFtPortalOnly>(variant);  // matte, portal lights only
+// ab: the build that counts the algorithmic path-state bytes (pt_set_count_bytes)
+static ShadeKernel shade_kernel(int variant, int features, bool ab = false) {
+    if (features == kFtPortalOnly) return shade_kernel_ft<kFtPortalOnly>(variant, ab);  // matte, portal lights only
     switch (features & kFtAll) {
-        case 0: return shade_kernel_ft<0>(variant);
-        case kFtInfinite: return shade_kernel_ft<kFtInfinite>(variant);
-        case kFtSphere: return shade_kernel_ft<kFtSphere>(variant);
-        case kFtInfinite | kFtSphere: return shade_kernel_ft<kFtInfinite | kFtSphere>(variant);
-        default: return shade_kernel_ft<kFtAll>(variant);
+        case 0: return shade_kernel_ft<0>(variant, ab);
+        case kFtInfinite: return shade_kernel_ft<kFtInfinite>(variant, ab);
+        case kFtSphere: return shade_kernel_ft<kFtSphere>(variant, ab);
+        case kFtInfinite | kFtSphere: return shade_kernel_ft<kFtInfinite | kFtSphere>(variant, ab);
+        default: return shade_kernel_ft<kFtAll>(variant, ab);
     }
 }
 
@@ -394,6 +398,10 @@ static TraceNbKernel trace_nb_kernel(bool lds, bool sph) {
                : (sph ? k_trace_nb<false, true> : k_trace_nb<false, false>);
 }
 static TraceNbKernel trace_lds_kernel(bool sph) { return sph ? k_trace_lds<true> : k_trace_lds<false>; }
+using TraceLds2Kernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, DevStats*);
+static TraceLds2Kernel trace_lds2_kernel(bool sph, int waves) {
+    return sph ? k_trace_lds2<true, 4> : (waves == 5 ? k_trace_lds2<false, 5> : k_trace_lds2<false, 4>);
+}
 using TracePtKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, int*,
                                DevStats*);
 static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
@@ -1099,7 +1107,7 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
 // scene (pt_scene_query PT_Q_TRACE_KERNEL / PT_Q_SHADE_KERNEL; the bench names
 // the kernel its roofline is for).
 static int trace_kernel_id(const pt_scene* s) {
-    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) return 3;
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) return s->trace_2r ? 4 : 3;
     if (s->trace_persist == 2 && !s->trace_spill) return 2;
     return s->trace_persist ? 1 : 0;
 }
@@ -1116,7 +1124,12 @@ static int shade_kernel_id(const pt_scene* s) {
 static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
                          hipStream_t st) {
     const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && s->trace_2r) {
+        // k_trace_lds2: two stack regions (one per ray slot) of k_trace_lds's rows
+        const size_t lds = s->lds_scene_bytes + (size_t)2 * (s->stack_rows + 2) * kTraceBlock * sizeof(int);
+        hipLaunchKernelGGL(trace_lds2_kernel(s->has_spheres, s->trace_2r_waves), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
+                           counts + 0, counts + 4, 2 * s->refill_min, 2 * s->leaf_min, s->stack_rows, w.stats.p);
+    } else if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
         // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
         hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
@@ -1347,7 +1360,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 } else {
                     const ShadeKernel kshade =
                         direct ? k_shade_dl<kFtAll>
-                               : shade_kernel(shade_variant_of(s), s->features);
+                               : shade_kernel(shade_variant_of(s), s->features, s->count_bytes);
                     hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
                                        pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
                 }
@@ -1620,6 +1633,10 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
     if (const char* t = std::getenv("PT_TRACE_LEAN")) s->trace_lean = t[0] != '0';
+    if (const char* t = std::getenv("PT_TRACE_2R")) {
+        s->trace_2r = t[0] == '1' || t[0] == '2';
+        s->trace_2r_waves = t[0] == '2' ? 5 : 4;
+    }
     if (std::getenv("PT_TRACE_DEBUG"))
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,
                      s->trace_spill, s->lds_scene_bytes,
@@ -1998,6 +2015,14 @@ pt_status pt_set_batch_slots(pt_scene* s, int64_t slots) {
                 throw PtError(PT_ERR_INVALID_ARG, "batch slots exceed a replica's path-state indexing limit");
         s->target_slots = (size_t)slots;
         for (auto& r : s->replicas) r->target_slots = (size_t)slots;
+    });
+}
+
+pt_status pt_set_count_bytes(pt_scene* s, int32_t on) {
+    return guarded([&] {
+        if (!s) throw PtError(PT_ERR_INVALID_ARG, "null scene");
+        s->count_bytes = on != 0;
+        for (auto& r : s->replicas) r->count_bytes = on != 0;
     });
 }
 

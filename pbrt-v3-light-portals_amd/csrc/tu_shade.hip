@@ -7,10 +7,14 @@
 
 namespace pt {
 #define PT_ARGS DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, DevStats*
-#define PT_SHADE_FT(F)                                \
-    template __global__ void k_shade<F>(PT_ARGS);     \
-    template __global__ void k_shade_tab<F>(PT_ARGS); \
-    template __global__ void k_shade_w3<F>(PT_ARGS);
+// each variant with and without the algorithmic-byte count (kAb)
+#define PT_SHADE_FT(F)                                       \
+    template __global__ void k_shade<F, false>(PT_ARGS);     \
+    template __global__ void k_shade_tab<F, false>(PT_ARGS); \
+    template __global__ void k_shade_w3<F, false>(PT_ARGS);  \
+    template __global__ void k_shade<F, true>(PT_ARGS);      \
+    template __global__ void k_shade_tab<F, true>(PT_ARGS);  \
+    template __global__ void k_shade_w3<F, true>(PT_ARGS);
 #if !defined(PT_FT) || PT_FT == 0
 PT_SHADE_FT(0)
 #endif

@@ -311,13 +311,17 @@ class Scene:
         if batch_slots:
             _check(lib().pt_set_batch_slots(self._s, int(batch_slots)))
 
+    def set_count_bytes(self, on: bool) -> None:
+        """pt_set_count_bytes: stats['shade_bytes'] counted in the renders that follow."""
+        _check(lib().pt_set_count_bytes(self._s, int(bool(on))))
+
     def set_pipelines(self, n: int) -> None:
         """pt_set_pipelines: batches in flight (1 = one after the other)."""
         _check(lib().pt_set_pipelines(self._s, int(n)))
 
     QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4,
                   "trace_kernel": 5, "shade_kernel": 6}
-    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds"}
+    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds", 4: "k_trace_lds2"}
     SHADE_KERNELS = {0: "k_shade", 3: "k_shade_w3", 5: "k_shade_tab", 6: "k_shade_dl", 7: "k_shade_hero",
                      8: "k_shade_hero_w2", 9: "k_shade_hero_w4"}
 

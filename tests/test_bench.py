@@ -53,8 +53,8 @@ def test_roofline_kernel_is_timed_dominant_and_traffic_needs_same_sources(tmp_pa
     pmc = {"workload": wl, "source_hash": "old", "kernels": {
         "void pt::k_shade_w3<16>": {"launches": 10, "hbm_bytes_per_launch": 2.0e10}}}
     (tmp_path / "profiles" / "r3_pmc_traffic.json").write_text(json.dumps(pmc))
-    timed = _timed(400.0, 500.0)          # shading dominates the timed region
-    iso = _timed(350.0, 270.0)            # ... though tracing dominates the isolated frame
+    timed = dict(_timed(400.0, 500.0), shade_bytes=0)  # shading dominates the timed region (bytes not counted there)
+    iso = _timed(350.0, 270.0)            # ... though tracing dominates the isolated frame, which counts the bytes
     out = bench.rooflines(timed, iso, wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new")
     roof = out["roofline"]
     assert roof["kernel"] == "k_shade_w3"

@@ -121,6 +121,8 @@ def _edge_rays(sc, n_rand, n_edge, seed, tmax):
 
 TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
     "k_trace_lds": {},
+    "k_trace_lds2": {"PT_TRACE_2R": "1"},
+    "k_trace_lds2_w5": {"PT_TRACE_2R": "2"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
     "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
@@ -240,7 +242,8 @@ def test_tile_groups_batching_equal(variant):
 
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}])
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_2R": "1"},
+                                 {"PT_TRACE_2R": "2"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
@@ -722,3 +725,18 @@ def test_full_config_sparse_tiles_bit_exact():
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+def test_count_bytes_build_renders_the_same(variant):
+    """pt_set_count_bytes switches to the shading build that counts the
+    algorithmic path-state bytes: the same image and counters, shade_bytes > 0
+    only when it is on."""
+    hs, sc = _scene(variant(**MINI))
+    a, sa = sc.render()
+    sc.set_count_bytes(True)
+    b, sb = sc.render()
+    sc.set_count_bytes(False)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert sa["shade_bytes"] == 0 and sb["shade_bytes"] > 0
+    for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests", "shade_launches"):
+        assert sa[k] == sb[k], k
