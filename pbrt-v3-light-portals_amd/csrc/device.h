@@ -173,6 +173,7 @@ __host__ __device__ inline TabLayout tab_layout(int n_prims, int n_mats, int n_l
 //               the hit words
 //   body  32 B  {L.xyz, hidx} {beta.xyz, etaScale}
 //   nee   64 B  the deferred EstimateDirect payload (kNee* offsets)
+//   Lfin  12 B  the radiance of a finished sample
 //   ray / rayA / rayB  32 B  {o.xyz, d.x} {d.yz, tMax, 0} (kernels.hip load_ray)
 struct DevPaths {
     int n;
@@ -183,6 +184,7 @@ struct DevPaths {
     float* rayA;        // 8n NEE ray A (MIS shadow ray: its tMax), same record
     float* rayB;        // 8n NEE ray B, same record
     float* nee;         // kNee floats per slot
+    float* Lfin;        // 3n: the finished sample's L (pixel-major, dense: what the film pass reads)
     // DirectLightingIntegrator only (null otherwise): see kDl* below
     int* dli;           // kDlInts * n
     float* dlf;         // kDlFloats * n

@@ -7,6 +7,7 @@
 namespace pt {
 
 constexpr int kTraceBlock = 128;       // 2 waves; LDS stack = kStackLds * 128 * 4 B
+constexpr int kOctBlock = 448;         // k_trace_oct: 7 waves per block, 4 blocks per CU
 constexpr uint32_t kTraceChunk = 512;  // ray-queue entries a k_trace_nb wave takes per atomic
 // k_trace_nb: node visits / primitive tests per loop iteration for lanes that
 // stay in node / leaf mode (the loop's refill and step-kind bookkeeping is paid

@@ -924,177 +924,103 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
 #endif
 
 // ----------------------------------------------------------------------------
-// k_trace_lds2: k_trace_lds with TWO rays per lane.  A node step of k_trace_lds
-// is one dependent chain (LDS node + stack top -> box test -> next address);
-// with one ray per lane only other waves hide its LDS and ALU latency.  Here
-// each lane carries ray slots 0 and 1, their node reads are issued together
-// under one wait, and both box tests run in one basic block (the step kind
-// and the per-slot `go` conditions are lane masks, not branches), so the two
-// chains interleave.  Each slot keeps its own LDS stack column (two stack
-// regions per block).  A slot's sequence of node visits, primitive tests and
-// tMax updates is k_trace_lds's, so hits and counters are the reference's.
+// k_trace_oct: k_trace_lds over per-octant node images.  Every box test of the
+// reference picks each slab's near and far plane by the ray's direction signs
+// (Bounds3::IntersectP with dirIsNeg, geometry.h:1584-1606) and BVHAccel
+// visits the near child first by the split axis' sign (bvh.cpp:700-712): both
+// choices depend only on the ray's octant.  A block therefore stages the BVH
+// eight times, once per octant, with each node's planes stored near/far and
+// its children stored near/far, and a ray walks the image of its octant: the
+// node step has no per-node selects, and each slab's two distances are one
+// packed pair (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations on both
+// halves, in the reference's order).  Node visits, primitive tests, tMax
+// updates and the box test's answers (NaN slabs included, as box_hit_mm) are
+// k_trace_lds's, so hits and counters are the reference's.
+//
+// Octant image node (32 B): {x_near, x_far, y_near, y_far} {z_near, z_far, Z, W}
+//   interior: Z = LDS address of the near child, W = of the far child (same image)
+//   leaf:     Z = 0x80000000 | primitive end, W = first primitive
+// Blocks of kOctBlock threads (7 waves: four blocks fill a CU at 7 waves per
+// SIMD) share one staging; the stack is k_trace_lds's LDS column of node
+// addresses, rows kOctBlock * 4 B apart.
 // ----------------------------------------------------------------------------
-struct Tr2 {
-    Ray ray;
-    V3 inv;
-    TriShear sh;
-    uint32_t sgn, sp, cur, slot, kind;
-    int hitPrim, leafPos, leafEnd;
-    bool active, n0, n1, n2;
-};
-__device__ __forceinline__ void tr2_start(Tr2& t, const DevScene& sc, const DevPaths& ps, uint32_t e, uint32_t node0,
-                                          uint32_t sbase, uint32_t* nrays) {
-    t.slot = e >> 2;
-    t.kind = e & 3u;
-    t.ray = load_ray_trace(t.kind == kRayCont ? ps.ray : (t.kind == kRayB ? ps.rayB : ps.rayA), t.slot,
-                           t.kind == kRayShadow);
-    t.inv = v3(1 / t.ray.d.x, 1 / t.ray.d.y, 1 / t.ray.d.z);
-    t.sh = tri_shear(t.ray.d);
-    t.n0 = t.inv.x < 0; t.n1 = t.inv.y < 0; t.n2 = t.inv.z < 0;
-    t.sgn = (t.n0 ? 1u << 16 : 0u) | (t.n1 ? 1u << 17 : 0u) | (t.n2 ? 1u << 18 : 0u);
-    t.cur = node0; t.sp = sbase; t.hitPrim = -1; t.leafPos = 0; t.leafEnd = 0;
-    t.active = sc.n_nodes > 0;  // empty scene: every ray misses
-    if (!t.active) {
-        if (t.kind == kRayShadow) *hit_word(ps, t.slot, kHdHitA) = 0;
-        else if (t.kind == kRayCont) *hit_word(ps, t.slot, kHdHit) = -1;
-        else if (t.kind == kRayA) *hit_word(ps, t.slot, kHdHitA) = -1;
-        else *hit_word(ps, t.slot, kHdHitB) = -1;
-    }
-    *nrays += t.kind == kRayShadow ? 0x10000u : 1u;
+typedef float pt_f2 __attribute__((ext_vector_type(2)));
+static_assert(kOctBlock * 4 == 1792, "k_trace_oct stack rows are 1792 bytes apart");
+__device__ __forceinline__ void lds_push_oct(uint32_t sp, int v) {
+    asm volatile("ds_write_b32 %0, %1 offset:1792" : : "v"(sp), "v"(v) : "memory");
 }
-__device__ __forceinline__ void tr2_finish(Tr2& t, const DevPaths& ps) {
-    if (t.kind == kRayShadow) *hit_word(ps, t.slot, kHdHitA) = t.hitPrim >= 0 ? 1 : 0;
-    else if (t.kind == kRayCont) *hit_word(ps, t.slot, kHdHit) = t.hitPrim;
-    else if (t.kind == kRayA) *hit_word(ps, t.slot, kHdHitA) = t.hitPrim;
-    else *hit_word(ps, t.slot, kHdHitB) = t.hitPrim;
-    t.active = false;
-}
-// up to kLeafSteps primitive tests of slot t's leaf; returns true when the ray is finished
-template <bool kSph>
-__device__ __forceinline__ bool tr2_leaf(Tr2& t, const DevScene& sc, const float4* bprims, uint32_t sbase,
-                                         uint32_t* prims) {
-    bool done = false;
-#pragma unroll
-    for (int u = 0; u < kLeafSteps; ++u) {
-        if (!(!done && t.leafPos < t.leafEnd)) continue;
-        const int pi = t.leafPos++;
-        ++*prims;
-        const float4 r0 = bprims[3 * pi];
-        const float4 r1 = bprims[3 * pi + 1];
-        const float4 r2 = bprims[3 * pi + 2];
-        const uint32_t fl = __float_as_uint(r0.w);
-        float tt = 0;
-        bool ok;
-        if (fl & kPrimAnalytic) {
-            ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), t.ray, &tt);
-        } else {
-            ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), t.ray, t.sh, &tt);
-            ok &= (t.kind == kRayShadow) | !(fl & kPrimDegenerate);
-        }
-        t.hitPrim = ok ? pi : t.hitPrim;
-        t.ray.tmax = (ok && t.kind != kRayShadow) ? tt : t.ray.tmax;
-        done = ok && t.kind == kRayShadow;
-        if (!done && t.leafPos == t.leafEnd) {  // the leaf is finished: pop
-            const bool empty = t.sp == sbase;
-            done = empty;
-            if (!empty) {
-                t.cur = (uint32_t)lds_top(t.sp);
-                t.sp -= 512;
-            }
-        }
-    }
-    return done;
-}
-// the two slots' nodes and stack tops, one wait
-__device__ __forceinline__ void lds_node_top2(uint32_t addr0, uint32_t sp0, uint32_t addr1, uint32_t sp1, float4* a0,
-                                              float4* b0, int* top0, float4* a1, float4* b1, int* top1) {
-    float4 x0, y0, x1, y1;
-    int t0, t1;
-    asm volatile(
-        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %6 offset:16\n\tds_read_b32 %2, %7\n\t"
-        "ds_read_b128 %3, %8\n\tds_read_b128 %4, %8 offset:16\n\tds_read_b32 %5, %9\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(y0), "=&v"(t0), "=&v"(x1), "=&v"(y1), "=&v"(t1)
-        : "v"(addr0), "v"(sp0), "v"(addr1), "v"(sp1)
-        : "memory");
-    *a0 = x0; *b0 = y0; *top0 = t0;
-    *a1 = x1; *b1 = y1; *top1 = t1;
-}
-// one node visit of slot t when go (lane mask), k_trace_lds's step with every
-// state update predicated on go; returns whether the ray finished
-__device__ __forceinline__ bool tr2_node(Tr2& t, bool go, float4 a, float4 b, int top, uint32_t sbase,
-                                         uint32_t* nodes) {
-    *nodes += go ? 1u : 0u;
-    const bool hit = box_hit_mm(a, b, t.ray, t.inv, t.n0, t.n1, t.n2);
-    const uint32_t off = __float_as_uint(b.z);  // leaf: primitivesOffset; interior: second child
-    const uint32_t w = __float_as_uint(b.w);
-    const bool inner = go & hit & ((int)w < 0);
-    const bool leaf = go & hit & ((int)w >= 0);
-    const bool neg = (w & t.sgn) != 0;
-    const bool empty = t.sp == sbase;
-    // the far child, written above the top whether or not it is kept (kept only for an interior node of a
-    // going slot; otherwise the row above the top is free)
-    lds_push(t.sp, (int)(neg ? t.cur + 32u : off));
-    const bool done = go & !hit & empty;
-    const bool pop = go & !hit & !empty;
-    t.cur = inner ? (neg ? off : t.cur + 32u) : (pop ? (uint32_t)top : t.cur);
-    t.sp = inner ? t.sp + 512 : (pop ? t.sp - 512 : t.sp);
-    t.leafPos = leaf ? (int)off : t.leafPos;
-    t.leafEnd = leaf ? (int)w : t.leafEnd;
-    return done;
+// The box test of box_hit_mm on an octant image node: px/py/pz the slabs' (near,
+// far) plane pairs, o / inv the ray's origin and reciprocal direction as splats
+__device__ __forceinline__ bool box_hit_oct(pt_f2 px, pt_f2 py, pt_f2 pz, V3 o, V3 inv, float tmax) {
+    const pt_f2 kx = {1.f, 1 + 2 * gammaf(3)};  // tMax *= 1 + 2 * gamma(3); the near distance times 1 exactly
+    const pt_f2 tx = ((px - o.x) * inv.x) * kx;  // scalar operands splat to both halves
+    const pt_f2 ty = ((py - o.y) * inv.y) * kx;
+    const pt_f2 tz = ((pz - o.z) * inv.z) * kx;
+    const float f0 = __builtin_fmaxf(__builtin_fmaxf(tx.x, ty.x), tz.x);
+    const float f1 = __builtin_fminf(__builtin_fminf(tx.y, ty.y), tz.y);
+    return !(f0 > f1) & (f0 < tmax) & (f1 > 0) & !__builtin_isunordered(tx.x, tx.y);
 }
 
-// kW: waves per SIMD the register budget is set for (4: no spill; 5: a 20-B spill)
-template <bool kSph, int kW>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kSph ? 1 : kW))) void k_trace_lds2(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
-                                                            const uint32_t* __restrict__ rq_count, uint32_t* fetch,
-                                                            int refill_min, int leaf_min, int stack_rows,
-                                                            DevStats* stats)
+template <bool kSph>
+__global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph ? 1 : 7))) void k_trace_oct(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq, const uint32_t* __restrict__ rq_count,
+    uint32_t* fetch, int refill_min, int leaf_min, DevStats* stats)
 #ifdef PT_TU_TRACE
 {
     extern __shared__ float4 lds_dyn[];
-    const int nn = 2 * sc.n_nodes;
-    const int scene_f4 = nn + 3 * sc.n_prims;
-    const uint32_t node0 = (uint32_t)(uintptr_t)lds_dyn;
-    for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
-        float4 v = i < nn ? sc.nodes[i] : sc.prims[i - nn];
-        if (i < nn && (i & 1)) {  // the node encoding of k_trace_lds
-            const uint32_t npax = __float_as_uint(v.w);
-            const uint32_t np = npax & 0xffffu;
-            const uint32_t off = (uint32_t)__float_as_int(v.z);
-            v.w = __uint_as_float(np ? off + np : 0x80000000u | (1u << (16 + (npax >> 16))));
-            if (!np) v.z = __uint_as_float(node0 + 32u * off);
+    const int nnodes = sc.n_nodes;
+    const int img_f4 = 2 * nnodes;           // float4s of one octant image
+    const int nprim_f4 = 3 * sc.n_prims;
+    const uint32_t img0 = (uint32_t)(uintptr_t)lds_dyn;
+    const uint32_t img_bytes = 32u * (uint32_t)nnodes;
+    // the eight octant images, then the primitive records (as k_trace_lds)
+    for (int i = threadIdx.x; i < 8 * nnodes; i += blockDim.x) {
+        const int o = i / nnodes, k = i - o * nnodes;
+        const float4 a = sc.nodes[2 * k], b = sc.nodes[2 * k + 1];
+        const bool n0 = o & 1, n1 = (o >> 1) & 1, n2 = (o >> 2) & 1;
+        // LinearBVHNode: a = {bmin.xyz, bmax.x}, b = {bmax.yz, offset, nPrimitives | axis << 16}
+        float4 A, B;
+        A.x = n0 ? a.w : a.x; A.y = n0 ? a.x : a.w;
+        A.z = n1 ? b.x : a.y; A.w = n1 ? a.y : b.x;
+        B.x = n2 ? b.y : a.z; B.y = n2 ? a.z : b.y;
+        const uint32_t npax = __float_as_uint(b.w);
+        const uint32_t np = npax & 0xffffu, axis = npax >> 16;
+        const uint32_t off = (uint32_t)__float_as_int(b.z);
+        const uint32_t base = img0 + (uint32_t)o * img_bytes;
+        if (np > 0) {
+            B.z = __uint_as_float(0x80000000u | (off + np));
+            B.w = __uint_as_float(off);
+        } else {
+            const bool neg = (o >> axis) & 1;  // dirIsNeg[axis]: the second child first
+            const uint32_t first = base + 32u * (uint32_t)(k + 1), second = base + 32u * off;
+            B.z = __uint_as_float(neg ? second : first);
+            B.w = __uint_as_float(neg ? first : second);
         }
-        lds_dyn[i] = v;
+        lds_dyn[(size_t)o * img_f4 + 2 * k] = A;
+        lds_dyn[(size_t)o * img_f4 + 2 * k + 1] = B;
     }
+    for (int i = threadIdx.x; i < nprim_f4; i += blockDim.x) lds_dyn[8 * img_f4 + i] = sc.prims[i];
     __syncthreads();
-    const float4* bprims = lds_dyn + nn;
-    // two stack regions of (stack_rows + 2) rows; the lane's column in each
-    const uint32_t srow = (uint32_t)(uintptr_t)((int*)(lds_dyn + scene_f4) + threadIdx.x);
-    const uint32_t sbase0 = srow, sbase1 = srow + (uint32_t)(stack_rows + 2) * 512u;
+    const float4* bprims = lds_dyn + 8 * img_f4;
+    // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
+    const uint32_t sbase = (uint32_t)(uintptr_t)((int*)(lds_dyn + 8 * img_f4 + nprim_f4) + threadIdx.x);
     const uint32_t n = *rq_count;
     const uint32_t lane = lane_id();
-    uint32_t nrays = 0, nodes = 0, prims = 0;
+    uint32_t nrays = 0, nodes = 0, prims = 0;  // nrays: closest + shadow << 16
     unsigned long long iters_w = 0;
-    bool exhausted = false, drained = false;
+    bool active = false, exhausted = false, drained = false;
     uint32_t qn = 0, qe = 0;
-    Tr2 t0, t1;
-    t0.ray = t1.ray = Ray{v3(0, 0, 0), v3(0, 0, 1), 0};
-    t0.inv = t1.inv = v3(0, 0, 0);
-    t0.sh = t1.sh = TriShear{0, 0, 0, 0};
-    t0.sgn = t1.sgn = 0;
-    t0.sp = sbase0; t1.sp = sbase1;
-    t0.cur = t1.cur = node0;
-    t0.slot = t1.slot = 0; t0.kind = t1.kind = 0;
-    t0.hitPrim = t1.hitPrim = -1;
-    t0.leafPos = t1.leafPos = t0.leafEnd = t1.leafEnd = 0;
-    t0.active = t1.active = false;
-    t0.n0 = t0.n1 = t0.n2 = t1.n0 = t1.n1 = t1.n2 = false;
+    uint32_t slot = 0, kind = 0;
+    Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
+    V3 inv = v3(0, 0, 0);
+    TriShear sh{0, 0, 0, 0};
+    uint32_t sp = sbase, cur = img0;
+    int hitPrim = -1, leafPos = 0, leafEnd = 0;
     for (;;) {
         if (!exhausted) {
-            const uint64_t idle0 = __ballot(!t0.active), idle1 = __ballot(!t1.active);
-            const uint32_t ni0 = (uint32_t)__popcll(idle0);
-            const uint32_t nidle = ni0 + (uint32_t)__popcll(idle1);
-            if (nidle >= (uint32_t)refill_min || nidle == 128u) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
@@ -1104,47 +1030,104 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(kSp
                     drained = base + kTraceChunk >= n;
                 }
                 const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
-                const uint32_t k0 = lanes_below(idle0), k1 = ni0 + lanes_below(idle1);
-                const uint32_t i0 = qn + k0, i1 = qn + k1;
+                const uint32_t k = lanes_below(idle);
+                const uint32_t i = qn + k;
                 qn += take;
                 if (drained && qn >= qe) exhausted = true;
-                if (!t0.active && k0 < take) tr2_start(t0, sc, ps, rq[i0], node0, sbase0, &nrays);
-                if (!t1.active && k1 < take) tr2_start(t1, sc, ps, rq[i1], node0, sbase1, &nrays);
+                if (!active && k < take) {
+                    const uint32_t e = rq[i];
+                    slot = e >> 2;
+                    kind = e & 3u;
+                    ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
+                    inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                    sh = tri_shear(ray.d);
+                    const uint32_t oct = (inv.x < 0 ? 1u : 0u) | (inv.y < 0 ? 2u : 0u) | (inv.z < 0 ? 4u : 0u);
+                    cur = img0 + oct * img_bytes; sp = sbase; hitPrim = -1; leafPos = 0; leafEnd = 0;
+                    active = nnodes > 0;  // empty scene: every ray misses
+                    if (!active) {
+                        if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
+                        else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = -1;
+                        else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
+                        else *hit_word(ps, slot, kHdHitB) = -1;
+                    }
+                    nrays += kind == kRayShadow ? 0x10000u : 1u;
+                }
             }
         }
-        const bool wl0 = t0.active && t0.leafPos < t0.leafEnd, wl1 = t1.active && t1.leafPos < t1.leafEnd;
-        const bool wn0 = t0.active && !wl0, wn1 = t1.active && !wl1;
-        const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wl0)) + (uint32_t)__popcll(__ballot(wl1));
-        const uint32_t nNode = (uint32_t)__popcll(__ballot(wn0)) + (uint32_t)__popcll(__ballot(wn1));
-        if ((nLeaf | nNode) == 0) {
+        const bool wantLeaf = active && leafPos < leafEnd;
+        const uint64_t mLeaf = __ballot(wantLeaf);
+        const uint64_t mNode = __ballot(active && !wantLeaf);
+        if ((mLeaf | mNode) == 0) {
             if (exhausted) break;
             continue;
         }
-        const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
         ++iters_w;
-        bool done0 = false, done1 = false;
+        bool done = false;
         if (leafStep) {
-            if (wl0) done0 = tr2_leaf<kSph>(t0, sc, bprims, sbase0, &prims);
-            if (wl1) done1 = tr2_leaf<kSph>(t1, sc, bprims, sbase1, &prims);
+#pragma unroll
+            for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
+                if (!(active && !done && leafPos < leafEnd)) continue;
+                const int pi = leafPos++;
+                ++prims;
+                const float4 r0 = bprims[3 * pi];
+                const float4 r1 = bprims[3 * pi + 1];
+                const float4 r2 = bprims[3 * pi + 2];
+                const uint32_t fl = __float_as_uint(r0.w);
+                float t = 0;
+                bool ok;
+                if (fl & kPrimAnalytic) {
+                    ok = shape_test<kSph>(sc, fl, __float_as_int(r1.w), ray, &t);
+                } else {
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
+                    ok &= (kind == kRayShadow) | !(fl & kPrimDegenerate);
+                }
+                hitPrim = ok ? pi : hitPrim;
+                ray.tmax = (ok && kind != kRayShadow) ? t : ray.tmax;
+                done = ok && kind == kRayShadow;
+                if (!done && leafPos == leafEnd) {  // the leaf is finished: pop
+                    const bool empty = sp == sbase;
+                    done = empty;
+                    if (!empty) {
+                        cur = (uint32_t)lds_top(sp);
+                        sp -= 1792;
+                    }
+                }
+            }
         } else {
-            // kNodeSteps node visits per loop iteration for the slots in node mode
 #pragma unroll
             for (int u = 0; u < kNodeSteps; ++u) {
-                const bool go0 = wn0 && !done0 && t0.leafPos >= t0.leafEnd;
-                const bool go1 = wn1 && !done1 && t1.leafPos >= t1.leafEnd;
-                if (!(go0 | go1)) continue;
-                float4 a0, b0, a1, b1;
-                int top0, top1;
-                lds_node_top2(t0.cur, t0.sp, t1.cur, t1.sp, &a0, &b0, &top0, &a1, &b1, &top1);
-                done0 |= tr2_node(t0, go0, a0, b0, top0, sbase0, &nodes);
-                done1 |= tr2_node(t1, go1, a1, b1, top1, sbase1, &nodes);
+                if (!(active && !done && leafPos >= leafEnd)) continue;
+                ++nodes;
+                float4 a, b;
+                int top;
+                lds_node_top(cur, sp, &a, &b, &top);
+                const bool hit = box_hit_oct(pt_f2{a.x, a.y}, pt_f2{a.z, a.w}, pt_f2{b.x, b.y}, ray.o, inv, ray.tmax);
+                const int Z = __float_as_int(b.z);
+                const uint32_t W = __float_as_uint(b.w);
+                const bool inner = hit & (Z >= 0);
+                const bool leaf = hit & (Z < 0);
+                const bool empty = sp == sbase;
+                lds_push_oct(sp, (int)W);  // the far child (kept only for an interior node)
+                done = !hit & empty;
+                const bool pop = !hit & !empty;
+                cur = inner ? (uint32_t)Z : (pop ? (uint32_t)top : cur);
+                sp = inner ? sp + 1792 : (pop ? sp - 1792 : sp);
+                leafPos = leaf ? (int)W : leafPos;
+                leafEnd = leaf ? (Z & 0x7fffffff) : leafEnd;
             }
         }
-        if (done0) tr2_finish(t0, ps);
-        if (done1) tr2_finish(t1, ps);
+        if (done) {
+            if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
+            else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
+            else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
+            else *hit_word(ps, slot, kHdHitB) = hitPrim;
+            active = false;
+        }
     }
     flush_stats(stats, nrays & 0xffffu, nrays >> 16, nodes, prims);
-    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 128ull * iters_w);
+    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
 }
 #else
 ;
@@ -1581,9 +1564,15 @@ __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t 
 __device__ __forceinline__ void store_L(const DevPaths& ps, uint32_t slot, S3 L) {
     *reinterpret_cast<float3*>(body_word(ps, slot, kBdL)) = make_float3(L.c[0], L.c[1], L.c[2]);
 }
-__device__ __forceinline__ S3 load_L(const DevPaths& ps, uint32_t slot) {
-    const float4 a = ps.body[2u * slot];
-    return s3(a.x, a.y, a.z);
+// A finished sample's radiance, pixel-major and dense (the film pass reads it
+// for every film pixel its filter footprint reaches)
+__device__ __forceinline__ void store_Lfin(const DevPaths& ps, uint32_t slot, S3 L) {
+    float* p = ps.Lfin + 3u * slot;
+    p[0] = L.c[0]; p[1] = L.c[1]; p[2] = L.c[2];
+}
+__device__ __forceinline__ S3 load_Lfin(const DevPaths& ps, uint32_t slot) {
+    const float* p = ps.Lfin + 3u * slot;
+    return s3(p[0], p[1], p[2]);
 }
 
 // ab: algorithmic path-state bytes this step reads and writes (the bench's
@@ -1728,9 +1717,10 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
             }
         }
     }
-    store_L(ps, slot, L);
     *st_word(ps, slot) = st;
     *keep = (st & (kStCont | kStNee)) != 0;
+    if (*keep) store_L(ps, slot, L);
+    else store_Lfin(ps, slot, L);
     if (ab) *ab += 4 * (rays->n + (*keep ? 1u : 0u));  // ray / path queue entries written
 }
 
@@ -2118,7 +2108,7 @@ __device__ __forceinline__ void shade_dl(const DevScene& sc, const DevPaths& ps,
             }
             case kDlReturn: {
                 if (d == 0) {
-                    store_L(ps, slot, Lc);
+                    store_Lfin(ps, slot, Lc);
                     step = kDlDone;
                     break;
                 }
@@ -2270,7 +2260,7 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
                                 const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
                                 touch = !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
                                 if (touch) {
-                                    S3 L = load_L(ps, slot);
+                                    S3 L = load_Lfin(ps, slot);
                                     if (has_nan(L)) L = s3(0.f);
                                     else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
                                     else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
@@ -2375,7 +2365,7 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
                                 y0 = (int)ceilf(dy - fc.ry); y1 = (int)floorf(dy + fc.ry) + 1;
                                 reach = !(gx1 < x0 || gx0 >= x1 || gy1 < y0 || gy0 >= y1);
                                 if (reach) {
-                                    L = load_L(ps, slot);
+                                    L = load_Lfin(ps, slot);
                                     if (has_nan(L)) L = s3(0.f);
                                     else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
                                     else if (__builtin_isinf(lum_y(L))) L = s3(0.f);

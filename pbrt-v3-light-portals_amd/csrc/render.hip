@@ -168,7 +168,7 @@ struct Work {
     DBuf<uint4> head;   // DevPaths records (device.h)
     DBuf<float4> body;
     DBuf<float2> pfilm;
-    DBuf<float> ray, rayA, rayB, nee;
+    DBuf<float> ray, rayA, rayB, nee, Lfin;
     DBuf<int> spill;
     DBuf<DevStats> stats;
     DBuf<int> dli;                 // DirectLighting state (kDl*)
@@ -211,7 +211,7 @@ struct Work {
         if (n > cap) {
             rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
             head.alloc(n); body.alloc(2 * n); pfilm.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
-            rayB.alloc(8 * n); nee.alloc((size_t)kNee * n);
+            rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); Lfin.alloc(3 * n);
             cap = n;
         }
         spill.alloc(spill_threads * 64);  // k_trace_pt: 64 words per lane (entries past its LDS rows)
@@ -224,6 +224,7 @@ struct Work {
         p.head = head.p; p.body = body.p; p.pfilm = pfilm.p;
         p.ray = ray.p; p.rayA = rayA.p; p.rayB = rayB.p;
         p.nee = nee.p;
+        p.Lfin = Lfin.p;
         p.dli = dl_frames > 0 ? dli.p : nullptr;
         p.dlf = dl_frames > 0 ? dlf.p : nullptr;
         p.dlframe = dl_frames > 0 ? dlframe.p : nullptr;
@@ -285,8 +286,7 @@ struct pt_scene {
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
-    bool trace_2r = false;       // k_trace_lds2: two rays per lane (PT_TRACE_2R=1: 4 waves per SIMD, =2: 5)
-    int trace_2r_waves = 4;
+    size_t oct_lds_bytes = 0;    // > 0: k_trace_oct (octant images of an LDS-sized BVH; opt-in PT_TRACE_OCT=1)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
@@ -398,10 +398,7 @@ static TraceNbKernel trace_nb_kernel(bool lds, bool sph) {
                : (sph ? k_trace_nb<false, true> : k_trace_nb<false, false>);
 }
 static TraceNbKernel trace_lds_kernel(bool sph) { return sph ? k_trace_lds<true> : k_trace_lds<false>; }
-using TraceLds2Kernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, DevStats*);
-static TraceLds2Kernel trace_lds2_kernel(bool sph, int waves) {
-    return sph ? k_trace_lds2<true, 4> : (waves == 5 ? k_trace_lds2<false, 5> : k_trace_lds2<false, 4>);
-}
+static TraceNbKernel trace_oct_kernel(bool sph) { return sph ? k_trace_oct<true> : k_trace_oct<false>; }
 using TracePtKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, int*,
                                DevStats*);
 static TracePtKernel trace_pt_kernel(bool lds, bool spill, bool sph) {
@@ -1107,7 +1104,8 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
 // scene (pt_scene_query PT_Q_TRACE_KERNEL / PT_Q_SHADE_KERNEL; the bench names
 // the kernel its roofline is for).
 static int trace_kernel_id(const pt_scene* s) {
-    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) return s->trace_2r ? 4 : 3;
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean)
+        return s->oct_lds_bytes ? 5 : 3;
     if (s->trace_persist == 2 && !s->trace_spill) return 2;
     return s->trace_persist ? 1 : 0;
 }
@@ -1124,11 +1122,11 @@ static int shade_kernel_id(const pt_scene* s) {
 static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
                          hipStream_t st) {
     const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && s->trace_2r) {
-        // k_trace_lds2: two stack regions (one per ray slot) of k_trace_lds's rows
-        const size_t lds = s->lds_scene_bytes + (size_t)2 * (s->stack_rows + 2) * kTraceBlock * sizeof(int);
-        hipLaunchKernelGGL(trace_lds2_kernel(s->has_spheres, s->trace_2r_waves), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
-                           counts + 0, counts + 4, 2 * s->refill_min, 2 * s->leaf_min, s->stack_rows, w.stats.p);
+    if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && s->oct_lds_bytes) {
+        // k_trace_oct: eight octant images of the BVH + the primitive records + the stack, 4 blocks per CU
+        const dim3 og(std::max(1, std::min(ceil_div(nrays, kOctBlock), s->num_cus * 4)));
+        hipLaunchKernelGGL(trace_oct_kernel(s->has_spheres), og, dim3(kOctBlock), s->oct_lds_bytes, st, s->dev, ps, rq,
+                           counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
     } else if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
         // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
@@ -1633,9 +1631,12 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
     if (const char* t = std::getenv("PT_TRACE_LEAN")) s->trace_lean = t[0] != '0';
-    if (const char* t = std::getenv("PT_TRACE_2R")) {
-        s->trace_2r = t[0] == '1' || t[0] == '2';
-        s->trace_2r_waves = t[0] == '2' ? 5 : 4;
+    {   // k_trace_oct when four blocks of it fit a CU's LDS (160 KB): octant images + primitives + stack
+        const size_t oct = 8 * 32 * (size_t)s->dev.n_nodes + 48 * (size_t)s->dev.n_prims +
+                           (size_t)(s->stack_rows + 2) * kOctBlock * sizeof(int);
+        const char* t = std::getenv("PT_TRACE_OCT");
+        s->oct_lds_bytes = (s->lds_scene_bytes && !s->trace_spill && 4 * oct <= 160 * 1024 && t && t[0] == '1')
+                               ? oct : 0;
     }
     if (std::getenv("PT_TRACE_DEBUG"))
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,

@@ -121,8 +121,7 @@ def _edge_rays(sc, n_rand, n_edge, seed, tmax):
 
 TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
     "k_trace_lds": {},
-    "k_trace_lds2": {"PT_TRACE_2R": "1"},
-    "k_trace_lds2_w5": {"PT_TRACE_2R": "2"},
+    "k_trace_oct": {"PT_TRACE_OCT": "1"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
     "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
@@ -242,8 +241,7 @@ def test_tile_groups_batching_equal(variant):
 
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_2R": "1"},
-                                 {"PT_TRACE_2R": "2"}])
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_OCT": "1"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
