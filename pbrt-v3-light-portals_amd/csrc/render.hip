@@ -291,6 +291,7 @@ struct pt_scene {
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
+    int batch_equal = 0;         // renders of at most this many batches get equal batches (PT_BATCH_EQUAL)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
     int leaf_min_pt = 16;        // k_trace_pt (HBM-resident BVHs): the same threshold
@@ -1218,7 +1219,19 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         int bx0, by0, bx1, by1;
     };
     std::vector<Group> groups;
-    const size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)64 << 20);
+    size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)64 << 20);
+    {   // a render of only a few batches (one rank's shard of a multi-GPU frame) is split into equal batches, a
+        // multiple of the pipelines, so the pipelines finish together instead of one running a short remainder
+        // batch alone (PT_BATCH_EQUAL=<max batches>, 0 = off)
+        const size_t total = (size_t)npix * (size_t)spp;
+        const size_t nb = (total + target - 1) / target;
+        const int pipes = std::max(1, std::min(s->pipes, kMaxPipes));
+        if (nb > 0 && (int)nb <= s->batch_equal) {
+            const size_t nbe = (nb + (size_t)pipes - 1) / (size_t)pipes * (size_t)pipes;
+            const size_t per_tile = (size_t)256 * (size_t)spp;  // whole 16x16 tiles
+            target = std::max(per_tile, ((total + nbe - 1) / nbe + per_tile - 1) / per_tile * per_tile);
+        }
+    }
     size_t max_slots = 0;
     for (size_t i = 0; i < tiles.size();) {
         size_t j = i;
@@ -1652,6 +1665,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN_PT")) s->leaf_min_pt = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("PT_BATCH_EQUAL")) s->batch_equal = std::max(0, std::atoi(t));
     if (const char* t = std::getenv("PT_PIPES")) s->pipes = std::max(1, std::min(kMaxPipes, std::atoi(t)));
     return s;
 }
