@@ -168,16 +168,18 @@ __host__ __device__ inline TabLayout tab_layout(int n_prims, int n_mats, int n_l
 // Per-path state for one batch of nslots camera samples, as per-slot records:
 // a path step's fields share a sector instead of one 4-B field per sector
 // (the path queue is compacted every bounce, so a wave's slots are spread).
-//   head  16 B  {st (kSt* bits, NEE flags at kStNfShift), hit, hitA, hitB}: the
-//               step's first load (what it reads next); the trace kernels write
-//               the hit words
+//   head  4 words {st (kSt* bits, NEE flags at kStNfShift), hit, hitA, hitB}:
+//               the step's first loads (what it reads next); the trace kernels
+//               write the hit words.  Kept as four SoA arrays (word k of slot s at
+//               k * n + s): a 4-B store that a record would share with 3 other
+//               slots' words shares its sector with 7 (C2 measured faster, C3 equal)
 //   body  32 B  {L.xyz, hidx} {beta.xyz, etaScale}
 //   nee   64 B  the deferred EstimateDirect payload (kNee* offsets)
 //   Lfin  12 B  the radiance of a finished sample
 //   ray / rayA / rayB  32 B  {o.xyz, d.x} {d.yz, tMax, 0} (kernels.hip load_ray)
 struct DevPaths {
     int n;
-    uint4* head;        // n
+    uint4* head;        // n: the four head-word arrays of n words each (st_word / hit_word)
     float4* body;       // 2n
     float2* pfilm;      // CameraSample::pFilm
     float* ray;         // 8n continuation ray
@@ -195,10 +197,10 @@ struct DevPaths {
 constexpr int kHdSt = 0, kHdHit = 1, kHdHitA = 2, kHdHitB = 3;
 constexpr int kBdL = 0, kBdHidx = 3, kBdBeta = 4, kBdEta = 7;
 __device__ __forceinline__ uint32_t* st_word(const DevPaths& ps, uint32_t slot) {
-    return reinterpret_cast<uint32_t*>(ps.head) + (4u * slot);
+    return reinterpret_cast<uint32_t*>(ps.head) + slot;
 }
 __device__ __forceinline__ int* hit_word(const DevPaths& ps, uint32_t slot, int k) {
-    return reinterpret_cast<int*>(ps.head) + (4u * slot + (uint32_t)k);
+    return reinterpret_cast<int*>(ps.head) + ((uint32_t)k * (uint32_t)ps.n + slot);
 }
 __device__ __forceinline__ float* body_word(const DevPaths& ps, uint32_t slot, int k) {
     return reinterpret_cast<float*>(ps.body) + (8u * slot + (uint32_t)k);

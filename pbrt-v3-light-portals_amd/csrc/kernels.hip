@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
         ps.body[2 * (size_t)slot + 1] = make_float4(1.f, 1.f, 1.f, 1.f);              // beta = 1, etaScale = 1
         // dims 0-4 (pFilm, time, pLens) and the wvl dimension consumed; with sample
         // arrays Get1D jumps over [5, arrayEndDim) for wvl (sampler.cpp:180-184)
-        ps.head[slot] = make_uint4((uint32_t)(sc.wvl_dim + 1) | kStCont, 0u, 0u, 0u);
+        *st_word(ps, slot) = (uint32_t)(sc.wvl_dim + 1) | kStCont;
         if (ps.dli) {
             ps.dli[kDlD * N + slot] = 0;
             ps.dli[kDlAoff * N + slot] = 0;
@@ -1544,7 +1544,6 @@ __device__ __forceinline__ void path_load_now(const DevScene& sc, const DevPaths
 // paths ahead, the body one path ahead and only what the head says this step
 // will read.
 __device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t slot, PathPre* p) {
-    // four 4-B loads from the one 16-B record (a uint4 load pins four aligned registers two paths ahead)
     p->st = *st_word(ps, slot);
     p->hit = *hit_word(ps, slot, kHdHit);
     p->hitA = *hit_word(ps, slot, kHdHitA);

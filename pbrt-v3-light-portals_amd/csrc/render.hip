@@ -2166,9 +2166,9 @@ pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, 
         launch_trace(s, w, ps, w.rq0.p, w.counts.p, (uint32_t)n, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipDeviceSynchronize());
-        // hit words of the head records (device.h): hit for closest-hit queries, hitA for any-hit ones
-        HIPCHK(hipMemcpy2D(out_prim, sizeof(int32_t), (const int*)w.head.p + (any ? kHdHitA : kHdHit), sizeof(uint4),
-                           sizeof(int32_t), (size_t)n, hipMemcpyDeviceToHost));
+        // the head's hit words (device.h): hit for closest-hit queries, hitA for any-hit ones
+        HIPCHK(hipMemcpy(out_prim, (const int*)w.head.p + (size_t)(any ? kHdHitA : kHdHit) * n, sizeof(int32_t) * n,
+                         hipMemcpyDeviceToHost));
         if (counters) {
             DevStats d;
             HIPCHK(hipMemcpy(&d, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
