@@ -46,4 +46,14 @@ struct FilmConsts {
     float table[256];
 };
 
+// k_film_sk's per-sample footprint record, which k_camera stores in place of
+// pFilm (DevPaths::pfilm as uint2) when win > 0: per axis, for the film pixel
+// offsets o = 0..2win (pixel q + o - win), the filter-table index (4 bits at
+// 4o) and whether AddSample's bounds reach it (bit 20 + o).  win <= 2.
+struct FilmMeta {
+    int win;  // 0: k_camera stores pFilm
+    float rx, ry, inv_rx, inv_ry;
+};
+constexpr int kFilmSkMaxWin = 2;
+
 }  // namespace pt

@@ -1152,9 +1152,27 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, float fx, float fy
     return xf_ray(sc.c2w, r);
 }
 
+// FilmMeta (kernels.h) of one axis: film pixel q + o - win for o = 0..2win against
+// AddSample's bounds and filter-table index (film.h:121-161) -- k_film's
+// expressions on the same pFilm coordinate
+__device__ __forceinline__ uint32_t film_meta_axis(float f, int q, int win, float r, float inv_r) {
+    const float d = f - 0.5f;
+    const int t0 = (int)ceilf(d - r), t1 = (int)floorf(d + r) + 1;
+    uint32_t m = 0;
+    for (int o = 0; o <= 2 * win; ++o) {
+        const int t = q + o - win;
+        if (t < t0 || t >= t1) continue;
+        int i = (int)floorf(fabsf((t - d) * inv_r * 16));
+        i = i < 15 ? i : 15;
+        m |= (uint32_t)i << (4 * o) | 1u << (20 + o);
+    }
+    return m;
+}
+
+template <bool kMeta>  // FilmMeta records (k_film_sk) instead of pFilm
 __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const int2* __restrict__ pix, int npix,
                                                 int s0, int nsamp, HaltonPixelConsts hp, uint32_t* rq,
-                                                uint32_t* pq)
+                                                uint32_t* pq, FilmMeta fm)
 #ifdef PT_TU_MISC
 {
     const uint32_t N = (uint32_t)ps.n;
@@ -1170,7 +1188,11 @@ __global__ __launch_bounds__(256) void k_camera(DevScene sc, DevPaths ps, const 
         float lx = 0.5f, ly = 0.5f;
         if (sc.lens_radius > 0) { lx = halton_dim(sc, idx, 3); ly = halton_dim(sc, idx, 4); }
         const Ray r = camera_ray(sc, fx, fy, lx, ly);
-        ps.pfilm[slot] = make_float2(fx, fy);
+        if (kMeta)
+            reinterpret_cast<uint2*>(ps.pfilm)[slot] = make_uint2(film_meta_axis(fx, px.x, fm.win, fm.rx, fm.inv_rx),
+                                                                  film_meta_axis(fy, px.y, fm.win, fm.ry, fm.inv_ry));
+        else
+            ps.pfilm[slot] = make_float2(fx, fy);
         ps.body[2 * (size_t)slot] = make_float4(0.f, 0.f, 0.f, __uint_as_float(idx));  // L = 0, hidx
         ps.body[2 * (size_t)slot + 1] = make_float4(1.f, 1.f, 1.f, 1.f);              // beta = 1, etaScale = 1
         // dims 0-4 (pFilm, time, pLens) and the wvl dimension consumed; with sample
@@ -2217,6 +2239,17 @@ __device__ __forceinline__ float lane_val(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
+// The radiance sanitiser of SamplerIntegrator::Render (integrator.cpp:592-613:
+// NaN, negative luminance, infinite luminance -> black) and AddSample's
+// maxSampleLuminance clamp (film.h:121-161).
+__device__ __forceinline__ S3 film_sanitize(S3 L, float max_lum) {
+    if (has_nan(L)) L = s3(0.f);
+    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
+    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
+    if (lum_y(L) > max_lum) L = L * (max_lum / lum_y(L));
+    return L;
+}
+
 __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
                                               int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum)
 #ifdef PT_TU_MISC
@@ -2259,11 +2292,7 @@ __global__ __launch_bounds__(256) void k_film(DevPaths ps, FilmConsts fc, const 
                                 const int y0 = (int)ceilf(dy - fc.ry), y1 = (int)floorf(dy + fc.ry) + 1;
                                 touch = !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
                                 if (touch) {
-                                    S3 L = load_Lfin(ps, slot);
-                                    if (has_nan(L)) L = s3(0.f);
-                                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
-                                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
-                                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                                    const S3 L = film_sanitize(load_Lfin(ps, slot), fc.max_lum);
                                     const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
                                     const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
                                     int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
@@ -2364,11 +2393,7 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
                                 y0 = (int)ceilf(dy - fc.ry); y1 = (int)floorf(dy + fc.ry) + 1;
                                 reach = !(gx1 < x0 || gx0 >= x1 || gy1 < y0 || gy0 >= y1);
                                 if (reach) {
-                                    L = load_Lfin(ps, slot);
-                                    if (has_nan(L)) L = s3(0.f);
-                                    else if ((double)lum_y(L) < -1e-5) L = s3(0.f);
-                                    else if (__builtin_isinf(lum_y(L))) L = s3(0.f);
-                                    if (lum_y(L) > fc.max_lum) L = L * (fc.max_lum / lum_y(L));
+                                    L = film_sanitize(load_Lfin(ps, slot), fc.max_lum);
                                 }
                             }
                             // the bounds relative to the square's corner, one byte each (|offset| <= 8 + win)
@@ -2411,6 +2436,177 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
         }
     }
     if (touched) accum[o] = acc;
+}
+#else
+;
+#endif
+
+// k_film_sk: the RGB film with one lane per film pixel and the lanes' walks
+// skewed so that lanes needing the same source pixel read it together.
+//
+// A film pixel's FilmTile sum is one serial chain (its window's source pixels
+// in scan order, each pixel's samples in order), so a film pass can only
+// choose which chains run side by side and when each reads its samples.
+// k_film gives a chain a wave (lane = sample, readlane-ordered adds); k_film_t
+// gives it a lane but walks every sample that reaches an 8 x 8 square, a
+// quarter of the lanes touching each.  Here a wave (one per block) owns
+// A x W film pixels (W = 2 win + 1 window rows, A = 64 / W columns: 12 x 5 for
+// the 2-pixel Gaussian) and lane (a, b) walks its own window -- step
+// k = 0..W^2-1 is source pixel (k mod W, k / W) of the window, all its samples
+// -- starting at step t0 of the wave's clock:
+//   skew 2: t0 = a + W b.  At clock t lane (a, b) reads source pixel
+//     (Fx - win + a + k mod W, Fy - win + b + k / W), k = t - t0, and
+//     a + k mod W + W (b + k / W) = t: every lane that needs a source pixel
+//     reads it at the same clock step, sample for sample, so the wave reads
+//     each source pixel of its region once (at most 64 / W + 1 distinct pixels
+//     per load instruction), over A + 2 W^2 - W - 1 steps;
+//   skew 1: t0 = a -- a source pixel is read once per window row that needs
+//     it, over A + W^2 - 1 steps;
+//   skew 0: no skew -- W^2 steps, every lane its own source pixel.
+// The kernel is bound by the lanes' serial walks (one wave per SIMD), so the
+// step count weighs against the loads shared.
+//
+// The per-sample footprint comes from k_camera's FilmMeta record (filter-table
+// index and reach per offset: AddSample's bounds and weight, film.h:121-161,
+// computed from pFilm as k_film computes them), and a sample's contribution is
+// formed without branches -- a sample that does not reach the lane's pixel
+// adds +0, which leaves a sum that starts at +0 bit-identical.  Sums per
+// FilmTile of the window (at most 2 x 2 tiles for win <= 2) are merged as XYZ
+// in tile order: k_film's operations in k_film's order, bit-identical.
+__global__ __launch_bounds__(64) void k_film_sk(DevPaths ps, FilmConsts fc, const int* __restrict__ pixslot, int p0,
+                                                int np, int nsamp, int bx0, int by0, int bw, int bh, float4* accum,
+                                                int skew)
+#ifdef PT_TU_MISC
+{
+    __shared__ float s_tab[256];
+    for (int i = (int)threadIdx.x; i < 256; i += 64) s_tab[i] = fc.table[i];
+    __syncthreads();
+    const int win = fc.win, W = 2 * win + 1, A = 64 / W;
+    const int lane = (int)lane_id();
+    const int b = lane / A, a = lane - b * A;
+    const int nbx = (bw + A - 1) / A, nby = (bh + W - 1) / W;
+    const int wv = (int)blockIdx.x;
+    if (wv >= nbx * nby) return;
+    const int tx = bx0 + (wv % nbx) * A + a, ty = by0 + (wv / nbx) * W + b;
+    const int wx0 = max(tx - win, fc.sb_x0), wx1 = min(tx + win, fc.sb_x1 - 1);
+    const int wy0 = max(ty - win, fc.sb_y0), wy1 = min(ty + win, fc.sb_y1 - 1);
+    const bool on = b < W && tx < bx0 + bw && ty < by0 + bh && wx0 <= wx1 && wy0 <= wy1;
+    const int tc0 = (wx0 - fc.sb_x0) >> 4, tr0 = (wy0 - fc.sb_y0) >> 4;
+    const int sbw = fc.sb_x1 - fc.sb_x0;
+    const int t0 = (skew >= 1 ? a : 0) + (skew >= 2 ? W * b : 0);
+    const int nsteps = W * W + (skew >= 1 ? A - 1 : 0) + (skew >= 2 ? W * (W - 1) : 0);
+    const bool clamp = fc.max_lum < __builtin_inff();  // maxSampleLuminance set (the default is infinite)
+    const float max_lum = fc.max_lum;
+    const uint2* __restrict__ meta = reinterpret_cast<const uint2*>(ps.pfilm);
+    const float* __restrict__ Lf = ps.Lfin;
+    float P[4][4];  // per window FilmTile (row-major 2 x 2): contribSum r, g, b, filterWeightSum
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P[i][0] = P[i][1] = P[i][2] = P[i][3] = 0.f;
+    uint32_t anyq = 0;
+    for (int t = 0; t < nsteps; ++t) {
+        const int k = t - t0;
+        const int ky = k >= 0 ? k / W : 0, kx = k - ky * W;
+        const int qx = tx + kx - win, qy = ty + ky - win;
+        int p = -1;
+        if (on && k >= 0 && k < W * W && qx >= wx0 && qx <= wx1 && qy >= wy0 && qy <= wy1)
+            p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
+        if (p >= 0 && p < np) {
+            const int quad = (((qy - fc.sb_y0) >> 4) - tr0) * 2 + (((qx - fc.sb_x0) >> 4) - tc0);
+            const uint32_t ox = (uint32_t)(tx - qx + win), oy = (uint32_t)(ty - qy + win);
+            const uint32_t sx = 4u * ox, sy = 4u * oy, rx = 20u + ox, ry = 20u + oy;
+            float c0 = quad == 0 ? P[0][0] : quad == 1 ? P[1][0] : quad == 2 ? P[2][0] : P[3][0];
+            float c1 = quad == 0 ? P[0][1] : quad == 1 ? P[1][1] : quad == 2 ? P[2][1] : P[3][1];
+            float c2 = quad == 0 ? P[0][2] : quad == 1 ? P[1][2] : quad == 2 ? P[2][2] : P[3][2];
+            float cw = quad == 0 ? P[0][3] : quad == 1 ? P[1][3] : quad == 2 ? P[2][3] : P[3][3];
+            uint32_t any = 0;
+            // sample contribution: (sanitised L) * w and w, or +0 where the sample does not reach the pixel
+            auto contrib = [&](uint2 m, float lr, float lg, float lb, float o[4]) {
+                const uint32_t touch = (m.x >> rx) & (m.y >> ry) & 1u;
+                S3 L = s3(lr, lg, lb);
+                float y = lum_y(L);
+                const bool zero = has_nan(L) || (double)y < -1e-5 || __builtin_isinf(y);
+                L = zero ? s3(0.f) : L;
+                y = zero ? 0.f : y;
+                if (clamp && y > max_lum) L = L * (max_lum / y);
+                const float w = s_tab[((m.y >> sy) & 15u) * 16u + ((m.x >> sx) & 15u)];
+                const S3 c = L * w;
+                o[0] = touch ? c.c[0] : 0.f;
+                o[1] = touch ? c.c[1] : 0.f;
+                o[2] = touch ? c.c[2] : 0.f;
+                o[3] = touch ? w : 0.f;
+                any |= touch;
+            };
+            auto add = [&](const float o[4]) {
+                c0 += o[0];
+                c1 += o[1];
+                c2 += o[2];
+                cw += o[3];
+            };
+            const uint32_t base = (uint32_t)p * (uint32_t)nsamp;
+            if ((nsamp & 3) == 0) {
+                // four samples per iteration (two 16-B meta loads, three 16-B radiance loads), the next
+                // four loaded before this four are formed; the four adds stay in sample order
+                const uint4* mp = reinterpret_cast<const uint4*>(meta + base);
+                const float4* lp = reinterpret_cast<const float4*>(Lf + 3u * base);
+                uint4 m01 = mp[0], m23 = mp[1];
+                float4 l0 = lp[0], l1 = lp[1], l2 = lp[2];
+                for (int s = 0; s < nsamp; s += 4) {
+                    uint4 n01 = m01, n23 = m23;
+                    float4 n0 = l0, n1 = l1, n2 = l2;
+                    if (s + 4 < nsamp) {
+                        const int g = (s >> 2) + 1;
+                        n01 = mp[2 * g];
+                        n23 = mp[2 * g + 1];
+                        n0 = lp[3 * g];
+                        n1 = lp[3 * g + 1];
+                        n2 = lp[3 * g + 2];
+                    }
+                    float o0[4], o1[4], o2[4], o3[4];
+                    contrib(make_uint2(m01.x, m01.y), l0.x, l0.y, l0.z, o0);
+                    contrib(make_uint2(m01.z, m01.w), l0.w, l1.x, l1.y, o1);
+                    contrib(make_uint2(m23.x, m23.y), l1.z, l1.w, l2.x, o2);
+                    contrib(make_uint2(m23.z, m23.w), l2.y, l2.z, l2.w, o3);
+                    add(o0);
+                    add(o1);
+                    add(o2);
+                    add(o3);
+                    m01 = n01; m23 = n23;
+                    l0 = n0; l1 = n1; l2 = n2;
+                }
+            } else {
+                for (int s = 0; s < nsamp; ++s) {
+                    const uint32_t slot = base + (uint32_t)s;
+                    float o[4];
+                    contrib(meta[slot], Lf[3u * slot], Lf[3u * slot + 1u], Lf[3u * slot + 2u], o);
+                    add(o);
+                }
+            }
+            if (any) anyq |= 1u << quad;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (quad == i) {
+                    P[i][0] = c0;
+                    P[i][1] = c1;
+                    P[i][2] = c2;
+                    P[i][3] = cw;
+                }
+            }
+        }
+        if (on && k == W * W - 1 && anyq) {
+            const size_t o = (size_t)(ty - fc.crop_y0) * (fc.crop_x1 - fc.crop_x0) + (tx - fc.crop_x0);
+            float4 acc = accum[o];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (!((anyq >> i) & 1u)) continue;
+                // RGBSpectrum::ToXYZ (spectrum.h:64-68) of the tile pixel, merged in tile order
+                acc.x += 0.412453f * P[i][0] + 0.357580f * P[i][1] + 0.180423f * P[i][2];
+                acc.y += 0.212671f * P[i][0] + 0.715160f * P[i][1] + 0.072169f * P[i][2];
+                acc.z += 0.019334f * P[i][0] + 0.119193f * P[i][1] + 0.950227f * P[i][2];
+                acc.w += P[i][3];
+            }
+            accum[o] = acc;
+        }
+    }
 }
 #else
 ;

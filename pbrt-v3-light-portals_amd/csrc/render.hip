@@ -291,6 +291,8 @@ struct pt_scene {
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
+    int film_sk = 0;             // RGB film, win <= 2: PT_FILM_SK=1 takes k_film_sk (skewed lane-per-pixel walks)
+    int film_skew = 1;           // k_film_sk: PT_FILM_SKEW=0/1/2 -- the lanes' walks unskewed / skewed by column / by column and row
     int batch_equal = 0;         // renders of at most this many batches get equal batches (PT_BATCH_EQUAL)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
     int leaf_min = 40;           // k_trace_nb: lanes parked at leaves that trigger a primitive-test step
@@ -1267,6 +1269,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     const int maxBlocksTrace = s->num_cus * 16;
     const int maxBlocksShade = s->num_cus * s->shade_bpc;
     const bool direct = s->dev.integrator == PT_INTEGRATOR_DIRECT;
+    // k_film_sk (RGB films with windows of 1-2 pixels) reads k_camera's footprint records instead of pFilm
+    FilmMeta fmeta{0, s->film.rx, s->film.ry, s->film.inv_rx, s->film.inv_ry};
+    if (s->film_sk && !s->hero && s->film.win >= 1 && s->film.win <= kFilmSkMaxWin) fmeta.win = s->film.win;
     // Batches run on `pipes` pipelines (host thread + stream + path-state
     // buffers each), dealt round-robin: while one batch traces, another
     // shades, so the latency-bound trace and shading kernels overlap on the
@@ -1340,8 +1345,8 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             const int s0 = batches[bi].s0;
             const int ns = std::min(g.S, s_end - s0);
             const uint32_t nb = (uint32_t)g.np * (uint32_t)ns;
-            hipLaunchKernelGGL(k_camera, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
-                               st, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p);
+            hipLaunchKernelGGL(fmeta.win > 0 ? k_camera<true> : k_camera<false>, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))), dim3(256), 0,
+                               st, s->dev, ps, dpix.p + g.p0, g.np, s0, ns, s->hpc, w.rq0.p, w.pq0.p, fmeta);
             if (s->hero)  // the hero wavelengths and 60-bin path state of every camera sample
                 hipLaunchKernelGGL(k_hero_init, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))),
                                    dim3(256), 0, st, s->dev, hh, ps, hps, nb);
@@ -1403,6 +1408,11 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 else if (s->hero)
                     hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, st, hh, ps, s->film, dslot.p, g.p0, g.np,
                                        ns, g.bx0, g.by0, bw, bh, d_accum);
+                else if (fmeta.win > 0)
+                    hipLaunchKernelGGL(k_film_sk, dim3(ceil_div(bw, 64 / (2 * fmeta.win + 1)) *
+                                                       ceil_div(bh, 2 * fmeta.win + 1)),
+                                       dim3(64), 0, st, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
+                                       d_accum, s->film_skew);
                 else if (s->film_t && s->film.win >= 2 && s->film.win <= 16)  // box (win 1): k_film is faster
                     hipLaunchKernelGGL(k_film_t, dim3(ceil_div(ceil_div(bw, 8) * ceil_div(bh, 8), 4)), dim3(256), 0, st, ps,
                                        s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);
@@ -1660,6 +1670,8 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                                                                                                    : "k_trace");
     if (const char* t = std::getenv("PT_FILM_BLK")) s->film_blk = std::atoi(t);
     if (const char* t = std::getenv("PT_FILM_T")) s->film_t = std::atoi(t);
+    if (const char* t = std::getenv("PT_FILM_SK")) s->film_sk = std::atoi(t);
+    if (const char* t = std::getenv("PT_FILM_SKEW")) s->film_skew = std::min(2, std::max(0, std::atoi(t)));
     if (const char* t = std::getenv("PT_SHADE_BPC")) s->shade_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_TRACE_BPC")) s->trace_bpc = std::max(1, std::min(64, std::atoi(t)));
     if (const char* t = std::getenv("PT_REFILL")) s->refill_min = std::max(1, std::atoi(t));

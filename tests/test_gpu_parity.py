@@ -707,6 +707,38 @@ def test_film_pixel_lanes_match_oracle(tmp_path, monkeypatch, filt, spp):
     assert np.array_equal(old.view(np.uint32), got.view(np.uint32))
 
 
+@pytest.mark.parametrize("filt,spp,skew", [("gaussian", 68, "1"), ("gaussian", 70, "2"), ("gaussian", 68, "0"),
+                                           ("gaussian", 68, "2"), ("box", 12, "1"), ("box", 9, "0"), ("box", 12, "2")])
+def test_film_skewed_lanes_match_oracle(tmp_path, monkeypatch, filt, spp, skew):
+    """k_film_sk (PT_FILM_SK=1: one lane per film pixel, the lanes' window
+    walks unskewed (0), skewed by column (1) or so that every lane needing a
+    source pixel reads it at the same step (2); the footprint from k_camera's
+    FilmMeta records): the 2-pixel Gaussian
+    of config 3 and the box filter, at sample counts that take the four-sample
+    loads (68, 12) and the one-sample loop (70, 9), under a crop window with an
+    odd film size and batches of two FilmTiles == the oracle's film bit for
+    bit, and == k_film."""
+    import re
+    from conftest import scene_variant
+    path = scene_variant(tmp_path, name="cornell_dielectric.pbrt", res=(45, 38), spp=spp)
+    txt = open(path).read().replace('Film "image"', 'Film "image" "float cropwindow" [0.07 0.95 0.12 0.9]')
+    if filt == "box":
+        txt = re.sub(r'PixelFilter "gaussian"\s*"float xwidth" \[2\]\s*"float ywidth" \[2\]', 'PixelFilter "box"', txt)
+    p = tmp_path / f"film_sk_{filt}.pbrt"
+    p.write_text(txt)
+    hs = ptgpu.HostScene(str(p))
+    slots = 16 * 16 * spp * 2
+    monkeypatch.setenv("PT_FILM_SK", "1")
+    monkeypatch.setenv("PT_FILM_SKEW", skew)
+    got, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
+    ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
+    assert ref[..., 3].max() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    monkeypatch.setenv("PT_FILM_SK", "0")
+    old, _ = ptgpu.Scene(hs, batch_slots=slots).render_accum(0, 1)
+    assert np.array_equal(old.view(np.uint32), got.view(np.uint32))
+
+
 def test_full_config_sparse_tiles_bit_exact():
     """Parity at the benchmarked configuration: the C2 scene as benchmarked
     (1920x1080 @256 spp, path maxdepth 5, the default 64 M-slot batches and
