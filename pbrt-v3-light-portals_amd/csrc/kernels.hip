@@ -2441,6 +2441,22 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
 ;
 #endif
 
+// k_film_prep: the batch's finished radiance sanitised in place before
+// k_film_sk reads it -- once per sample, where the film pass would repeat it
+// for every film pixel the sample reaches (film_sanitize, above).
+__global__ __launch_bounds__(256) void k_film_prep(DevPaths ps, float max_lum, uint32_t n)
+#ifdef PT_TU_MISC
+{
+    for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n; slot += gridDim.x * blockDim.x) {
+        const S3 L = film_sanitize(load_Lfin(ps, slot), max_lum);
+        float* p = ps.Lfin + 3u * slot;
+        p[0] = L.c[0]; p[1] = L.c[1]; p[2] = L.c[2];
+    }
+}
+#else
+;
+#endif
+
 // k_film_sk: the RGB film with one lane per film pixel and the lanes' walks
 // skewed so that lanes needing the same source pixel read it together.
 //
@@ -2468,7 +2484,8 @@ __global__ __launch_bounds__(256) void k_film_t(DevPaths ps, FilmConsts fc, cons
 //
 // The per-sample footprint comes from k_camera's FilmMeta record (filter-table
 // index and reach per offset: AddSample's bounds and weight, film.h:121-161,
-// computed from pFilm as k_film computes them), and a sample's contribution is
+// computed from pFilm as k_film computes them), the radiance is sanitised
+// beforehand by k_film_prep, and a sample's contribution is
 // formed without branches -- a sample that does not reach the lane's pixel
 // adds +0, which leaves a sum that starts at +0 bit-identical.  Sums per
 // FilmTile of the window (at most 2 x 2 tiles for win <= 2) are merged as XYZ
@@ -2495,8 +2512,6 @@ __global__ __launch_bounds__(64) void k_film_sk(DevPaths ps, FilmConsts fc, cons
     const int sbw = fc.sb_x1 - fc.sb_x0;
     const int t0 = (skew >= 1 ? a : 0) + (skew >= 2 ? W * b : 0);
     const int nsteps = W * W + (skew >= 1 ? A - 1 : 0) + (skew >= 2 ? W * (W - 1) : 0);
-    const bool clamp = fc.max_lum < __builtin_inff();  // maxSampleLuminance set (the default is infinite)
-    const float max_lum = fc.max_lum;
     const uint2* __restrict__ meta = reinterpret_cast<const uint2*>(ps.pfilm);
     const float* __restrict__ Lf = ps.Lfin;
     float P[4][4];  // per window FilmTile (row-major 2 x 2): contribSum r, g, b, filterWeightSum
@@ -2519,15 +2534,11 @@ __global__ __launch_bounds__(64) void k_film_sk(DevPaths ps, FilmConsts fc, cons
             float c2 = quad == 0 ? P[0][2] : quad == 1 ? P[1][2] : quad == 2 ? P[2][2] : P[3][2];
             float cw = quad == 0 ? P[0][3] : quad == 1 ? P[1][3] : quad == 2 ? P[2][3] : P[3][3];
             uint32_t any = 0;
-            // sample contribution: (sanitised L) * w and w, or +0 where the sample does not reach the pixel
+            // sample contribution: L * w and w (L sanitised by k_film_prep), or +0 where the sample does not
+            // reach the pixel
             auto contrib = [&](uint2 m, float lr, float lg, float lb, float o[4]) {
                 const uint32_t touch = (m.x >> rx) & (m.y >> ry) & 1u;
-                S3 L = s3(lr, lg, lb);
-                float y = lum_y(L);
-                const bool zero = has_nan(L) || (double)y < -1e-5 || __builtin_isinf(y);
-                L = zero ? s3(0.f) : L;
-                y = zero ? 0.f : y;
-                if (clamp && y > max_lum) L = L * (max_lum / y);
+                const S3 L = s3(lr, lg, lb);
                 const float w = s_tab[((m.y >> sy) & 15u) * 16u + ((m.x >> sx) & 15u)];
                 const S3 c = L * w;
                 o[0] = touch ? c.c[0] : 0.f;

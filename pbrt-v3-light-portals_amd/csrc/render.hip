@@ -291,7 +291,8 @@ struct pt_scene {
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
-    int film_sk = 0;             // RGB film, win <= 2: PT_FILM_SK=1 takes k_film_sk (skewed lane-per-pixel walks)
+    int film_sk = -1;            // RGB film: k_film_sk (skewed lane-per-pixel walks) for win 2 (-1, default: C3's 2-pixel
+                                 // Gaussian 20.5 -> 5.1 ms per launch), PT_FILM_SK=1 also for win 1 (box: equal), 0 never
     int film_skew = 1;           // k_film_sk: PT_FILM_SKEW=0/1/2 -- the lanes' walks unskewed / skewed by column / by column and row
     int batch_equal = 0;         // renders of at most this many batches get equal batches (PT_BATCH_EQUAL)
     int refill_min = 16;         // idle lanes that trigger a refill from the wave's queue chunk
@@ -1271,7 +1272,8 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     const bool direct = s->dev.integrator == PT_INTEGRATOR_DIRECT;
     // k_film_sk (RGB films with windows of 1-2 pixels) reads k_camera's footprint records instead of pFilm
     FilmMeta fmeta{0, s->film.rx, s->film.ry, s->film.inv_rx, s->film.inv_ry};
-    if (s->film_sk && !s->hero && s->film.win >= 1 && s->film.win <= kFilmSkMaxWin) fmeta.win = s->film.win;
+    const bool sk = s->film_sk > 0 || (s->film_sk < 0 && !s->film_t);  // an explicit PT_FILM_T=1 keeps k_film_t
+    if (!s->hero && sk && s->film.win >= (s->film_sk > 0 ? 1 : 2) && s->film.win <= kFilmSkMaxWin) fmeta.win = s->film.win;
     // Batches run on `pipes` pipelines (host thread + stream + path-state
     // buffers each), dealt round-robin: while one batch traces, another
     // shades, so the latency-bound trace and shading kernels overlap on the
@@ -1408,11 +1410,14 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                 else if (s->hero)
                     hipLaunchKernelGGL(k_film_s60, fg, dim3(256), 0, st, hh, ps, s->film, dslot.p, g.p0, g.np,
                                        ns, g.bx0, g.by0, bw, bh, d_accum);
-                else if (fmeta.win > 0)
+                else if (fmeta.win > 0) {
+                    hipLaunchKernelGGL(k_film_prep, dim3(std::max(1, std::min(ceil_div(nb, 256), s->num_cus * 16))),
+                                       dim3(256), 0, st, ps, s->film.max_lum, nb);
                     hipLaunchKernelGGL(k_film_sk, dim3(ceil_div(bw, 64 / (2 * fmeta.win + 1)) *
                                                        ceil_div(bh, 2 * fmeta.win + 1)),
                                        dim3(64), 0, st, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh,
                                        d_accum, s->film_skew);
+                }
                 else if (s->film_t && s->film.win >= 2 && s->film.win <= 16)  // box (win 1): k_film is faster
                     hipLaunchKernelGGL(k_film_t, dim3(ceil_div(ceil_div(bw, 8) * ceil_div(bh, 8), 4)), dim3(256), 0, st, ps,
                                        s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);

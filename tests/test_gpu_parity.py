@@ -739,6 +739,25 @@ def test_film_skewed_lanes_match_oracle(tmp_path, monkeypatch, filt, spp, skew):
     assert np.array_equal(old.view(np.uint32), got.view(np.uint32))
 
 
+@pytest.mark.parametrize("film_sk", ["1", "0"])
+def test_film_max_sample_luminance_matches_oracle(tmp_path, monkeypatch, film_sk):
+    """A finite Film "maxsampleluminance" (AddSample's clamp, film.h:121-161,
+    after the radiance sanitiser, integrator.cpp:592-613) with the 2-pixel
+    Gaussian: k_film_prep + k_film_sk (the default for this window) and k_film
+    == the oracle's film bit for bit."""
+    from conftest import scene_variant
+    path = scene_variant(tmp_path, name="cornell_dielectric.pbrt", res=(40, 34), spp=16)
+    txt = open(path).read().replace('Film "image"', 'Film "image" "float maxsampleluminance" [0.35]')
+    p = tmp_path / "film_maxlum.pbrt"
+    p.write_text(txt)
+    hs = ptgpu.HostScene(str(p))
+    monkeypatch.setenv("PT_FILM_SK", film_sk)
+    got, _ = ptgpu.Scene(hs, batch_slots=16 * 16 * 16 * 2).render_accum(0, 1)
+    ref, _ = pyoracle.render_accum(hs.desc, nthreads=8)
+    assert ref[..., 3].max() > 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
 def test_full_config_sparse_tiles_bit_exact():
     """Parity at the benchmarked configuration: the C2 scene as benchmarked
     (1920x1080 @256 spp, path maxdepth 5, the default 64 M-slot batches and
