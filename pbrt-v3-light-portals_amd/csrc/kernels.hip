@@ -383,7 +383,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
+                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
+                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -811,7 +811,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
+                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
+                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
