@@ -363,6 +363,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
     }
     int* stk = (int*)(lds_dyn + scene_f4);  // [row][kTraceBlock]
     const uint32_t n = *rq_count;
+    const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
+    const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
     int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle > 0 && (nidle >= (uint32_t)refill_min || nidle == 64u)) {
+            if (nidle >= rmin) {  // rmin in [1, 64]: one scalar compare
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
         const bool wantLeaf = active && leafPos < leafEnd;
         const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wantLeaf));
         const uint32_t nNode = (uint32_t)__popcll(__ballot(active && !wantLeaf));
-        const bool leafStep = nLeaf > 0 && (nNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        const bool leafStep = nLeaf >= (nNode == 0 ? 1u : lmin);  // lmin >= 1
         ++iters;
         if (!active || wantLeaf != leafStep) continue;
         bool done = false;
@@ -552,6 +554,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
     }
     int* stk = (int*)(lds_dyn + scene_f4) + threadIdx.x;  // entry k at stk[k * kTraceBlock]
     const uint32_t n = *rq_count;
+    const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
+    const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
     const uint32_t lane = lane_id();
     uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;
     bool active = false, exhausted = false, drained = false;
@@ -569,7 +573,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
+            if (nidle >= rmin) {  // rmin in [1, 64]: one scalar compare
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
             continue;
         }
         const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
-        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= lmin);
         ++iters;
         bool done = false;
         if (leafStep) {
@@ -791,6 +795,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
     // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
     const uint32_t sbase = (uint32_t)(uintptr_t)((int*)(lds_dyn + scene_f4) + threadIdx.x);
     const uint32_t n = *rq_count;
+    const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
+    const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
     const uint32_t lane = lane_id();
     uint32_t nrays = 0, nodes = 0, prims = 0;  // nrays: closest + shadow << 16
     unsigned long long iters_w = 0;  // wave total
@@ -807,7 +813,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
+            if (nidle >= rmin) {  // rmin in [1, 64]: one scalar compare
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
@@ -850,7 +856,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             continue;
         }
         const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
-        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= lmin);
         ++iters_w;
         bool done = false;
         if (leafStep) {
@@ -1005,6 +1011,8 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
     // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
     const uint32_t sbase = (uint32_t)(uintptr_t)((int*)(lds_dyn + 8 * img_f4 + nprim_f4) + threadIdx.x);
     const uint32_t n = *rq_count;
+    const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
+    const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
     const uint32_t lane = lane_id();
     uint32_t nrays = 0, nodes = 0, prims = 0;  // nrays: closest + shadow << 16
     unsigned long long iters_w = 0;
@@ -1020,7 +1028,7 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= (uint32_t)refill_min || nidle == 64u) {
+            if (nidle >= rmin) {  // rmin in [1, 64]: one scalar compare
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
@@ -1062,7 +1070,7 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
             continue;
         }
         const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
-        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= (uint32_t)leaf_min);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= lmin);
         ++iters_w;
         bool done = false;
         if (leafStep) {
