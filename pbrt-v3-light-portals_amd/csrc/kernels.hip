@@ -890,10 +890,14 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 }
             }
         } else {
-            // kNodeSteps node visits per loop iteration for lanes that stay in node mode
+            // kNodeSteps node visits per loop iteration for lanes that stay in node mode.  One lane mask,
+            // nm, tracks "still in node mode" (an interior node or a pop); done is derived once after the
+            // steps -- left node mode without a leaf -- instead of being merged after every step
+            const bool nm0 = active & (leafPos >= leafEnd);  // done is false here
+            bool nm = nm0;
 #pragma unroll
             for (int u = 0; u < kNodeSteps; ++u) {
-                if (!(active && !done && leafPos >= leafEnd)) continue;
+                if (!nm) continue;
                 ++nodes;
                 float4 a, b;
                 int top;
@@ -906,13 +910,14 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 const bool neg = (w & sgn) != 0;
                 const bool empty = sp == sbase;
                 lds_push(sp, (int)(neg ? cur + 32u : off));  // the far child (kept only for an interior node)
-                done = !hit & empty;
                 const bool pop = !hit & !empty;
+                nm = inner | pop;
                 cur = inner ? (neg ? off : cur + 32u) : (pop ? (uint32_t)top : cur);
                 sp = inner ? sp + 512 : (pop ? sp - 512 : sp);
                 leafPos = leaf ? (int)off : leafPos;
                 leafEnd = leaf ? (int)w : leafEnd;
             }
+            done = nm0 & !nm & (leafPos >= leafEnd);  // the ray left the BVH: stack empty on a miss
         }
         if (done) {
             if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
