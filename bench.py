@@ -98,7 +98,26 @@ REFERENCE_PROBE = {"value": 0.684, "unit": "Msamples/s", "cores": 8,
                              "draft C2 scene at 480x270 @16 spp scaled to the frame (not re-run here)"}
 
 
-def cpu_baseline(scene_path: str, seconds: float):
+def _progress(msg: str) -> None:
+    """A line on stderr between phases (long CPU phases -- a 10 M-triangle scene's load and the oracle's
+    BVH build -- would otherwise leave a GPU job silent for minutes)."""
+    print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(period: float = 30.0) -> None:
+    """A daemon thread that prints a line on stderr every `period` seconds: a 10 M-triangle scene's first
+    frame (host subdivision + SAH build inside the library call) runs for minutes without returning."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period)
+            _progress("still running")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def cpu_baseline(scene_path: str, seconds: float, hs=None):
     """Reference CPU path restated in C (oracle/, 'port'), timed on this host's
     cores on a bounded sample of the same frame: the 16x16 tiles t with
     t % stride == 0, spread over the whole image (stride sized so the timed
@@ -106,7 +125,8 @@ def cpu_baseline(scene_path: str, seconds: float):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import ptgpu
-    hs = ptgpu.HostScene(scene_path)
+    if hs is None:
+        hs = ptgpu.HostScene(scene_path)
     # Every core this process may run on, up to the box's declared CPU share
     # (OMP_NUM_THREADS: the GPU box gives one GPU's job 16 of the host's CPUs,
     # os.cpu_count() reports the whole machine)
@@ -116,12 +136,14 @@ def cpu_baseline(scene_path: str, seconds: float):
     w, h = hs.film_size()
     ntiles = ((w + 15) // 16) * ((h + 15) // 16)
     stride = max(1, ntiles // (2 * threads))
+    _progress(f"cpu baseline: calibration run (tile stride {stride}, {threads} threads)")
     t0 = time.perf_counter()
     _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
     per_tile = st["samples"] / max(1, (ntiles + stride - 1) // stride)
     want = max(2 * threads, min(ntiles, st["samples"] / dt * seconds / per_tile))
     stride = max(1, int(ntiles // want))
+    _progress(f"cpu baseline: timed run (tile stride {stride})")
     t0 = time.perf_counter()
     film, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
     dt = time.perf_counter() - t0
@@ -342,8 +364,11 @@ def main():
     spath = os.path.join(tmpdir, f"bench_scene_{os.getpid()}.pbrt")
     with open(spath, "w") as f:
         f.write(scene_text(args))
+    _heartbeat()
+    _progress(f"loading {args.config}")
     hs = ptgpu.HostScene(spath)
     sc = ptgpu.Scene(hs, device=local, batch_slots=args.batch_slots or None)
+    _progress("scene on the device; warmup")
     w, h = sc.film_size()
     lds_scene = sc.query("trace_lds_bytes") > 0  # the library stages this BVH in LDS (PT_TRACE_LDS honoured)
     names = sc.kernel_names()
@@ -368,6 +393,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    _progress(f"timed region: {args.steps} steps")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -404,6 +430,7 @@ def main():
     # with another's shading).  This rank's shard, no collective.
     iso = {"trace_ms": 0.0, "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0,
            "node_visits": 0, "prim_tests": 0}
+    _progress("isolated and byte-counting frames")
     pipes = sc.query("pipelines")
     sc.set_pipelines(1)
     accum.zero_()
@@ -463,8 +490,9 @@ def main():
         out["source_hash"] = src
         out.update(rooflines(agg, iso, workload, args.config, lds_scene, names, src))
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds)
+            out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds, hs)
             if not args.no_parity:
+                _progress("parity: the sampled tiles on the GPU")
                 out["parity"] = parity_check(sc, hs, stride, ref_acc, ref_st)
         if emul is not None:
             out["emulated_scaling"] = emul
