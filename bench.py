@@ -235,22 +235,35 @@ def sq_issue_view(config: str, kernel: str, src: str):
     return None
 
 
-def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: bool, names: tuple, src: str) -> dict:
-    """roofline = the kernel that dominates the TIMED region (HIP events on
-    its stream around every launch of the K timed steps, two pipelines
-    overlapping); both kernels' figures under roofline_kernels, with their
-    per-launch times in the timed region (what rocprofv3 --stats averages)
-    and in one isolated frame (batches one after the other).
+class RooflineBoundError(RuntimeError):
+    """The dominant kernel's time per frame exceeds the step it is part of."""
+
+
+def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: bool, names: tuple, src: str,
+              ms_per_step: float | None = None) -> dict:
+    """roofline = the kernel with the most time per frame in the ISOLATED
+    frame (pt_set_pipelines(1): the batches one after the other, so a launch's
+    HIP-event span is that kernel's own duration -- what a rocprofv3
+    --kernel-trace --stats pass at PT_PIPES=1 averages).  `achieved` and `frac`
+    come from that isolated per-launch time.  In the timed steps two pipelines
+    overlap one batch's trace with another's shading, so a timed launch span
+    includes the co-running kernel: those spans are reported only as
+    `overlapped_span_ms`.  Both kernels' figures are under roofline_kernels.
 
     * traversal: algorithmic bytes per SURVEY 8(d), 32 B per LinearBVHNode
       visit (bvh.cpp:95-104) + 48 B per primitive test (triangle.cpp:189-425),
       counted on the device.  For a scene whose BVH sits in LDS (C2-C4) those
-      are LDS reads: set against the ds_read_b128 aggregate (MI355X_MICROARCH
-      LDS table, ~150 TB/s), with the SQ issue view beside it.
+      are LDS reads: bound "lds/issue", set against the ds_read_b128 aggregate
+      (MI355X_MICROARCH LDS table, ~150 TB/s) with the SQ issue shares beside
+      it, and the shading kernel's HBM fraction as the line's `hbm_view`.
     * shading: the path-state bytes each path step must read and write (the
       state PathIntegrator::Li carries between vertices + queue entries),
       counted on the device per step (kernels.hip shade_path) in the extra
-      frame (pt_set_count_bytes)."""
+      frame (pt_set_count_bytes).
+
+    With ms_per_step given, the dominant kernel's isolated time per frame
+    must not exceed the step (5 % tolerance for clock drift between the two
+    measurements): RooflineBoundError otherwise."""
     trace_name, shade_name = names
     ks = {}
     # algorithmic bytes per launch: the trace counters of the timed steps; the shading kernel's count from the
@@ -261,19 +274,20 @@ def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: boo
         parts.append(("k_shade", shade_name, "shade",
                       float(iso["shade_bytes"]) / max(1, iso.get("shade_launches_counted", iso["shade_launches"]))))
     for key, kname, p, alg in parts:
-        nl = max(1, timed[p + "_launches"])
-        avg = timed[p + "_ms"] / nl
         il = max(1, iso[p + "_launches"])
+        avg = iso[p + "_ms"] / il  # isolated: the kernel's own duration per launch
+        span = timed[p + "_ms"] / max(1, timed[p + "_launches"])
         trf, trf_src, stale = pmc_traffic(workload, kname, src)
-        e = {"kernel": kname, "launches": timed[p + "_launches"], "avg_launch_ms": round(avg, 4),
-             "isolated_avg_launch_ms": round(iso[p + "_ms"] / il, 4),
+        e = {"kernel": kname, "launches_per_frame": iso[p + "_launches"], "avg_launch_ms": round(avg, 4),
+             "per_frame_ms": round(iso[p + "_ms"], 3),
+             "overlapped_span_ms": round(span, 4),
              "algorithmic_bytes_per_launch": round(alg, 1),
              "algorithmic_GBs": round(alg / (avg * 1e-3) / 1e9, 1) if avg > 0 else 0.0,
              "data": ("LDS (BVH + primitives staged per block)" if (p == "trace" and lds_scene) else
                       ("HBM (path state)" if p == "shade" else "HBM")),
              "hbm_traffic_per_launch": round(trf, 1) if trf is not None else None,
              "hbm_GBs": round(trf / (avg * 1e-3) / 1e9, 1) if (trf is not None and avg > 0) else None,
-             "traffic_source": trf_src, "total_ms": round(timed[p + "_ms"], 2)}
+             "traffic_source": trf_src}
         if trf is not None:
             e["traffic_over_algorithmic"] = round(trf / alg, 3) if alg > 0 else None
         if stale:
@@ -285,23 +299,43 @@ def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: boo
             iv = sq_issue_view(config, kname, src)
             if iv:
                 e["issue_view"] = iv
+        else:
+            e["hbm_view"] = {"achieved": e["algorithmic_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(e["algorithmic_GBs"] / HBM_PEAK_GBS, 5)}
         ks[key] = e
-    dom = max(ks, key=lambda k: ks[k]["total_ms"])
+    dom = max(ks, key=lambda k: ks[k]["per_frame_ms"])
     k = ks[dom]
     on_chip = dom == "k_trace" and lds_scene
-    achieved = k["hbm_GBs"] if on_chip else k["algorithmic_GBs"]
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved is not None else None,
-            "traffic": k["hbm_traffic_per_launch"], "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + "
-            "WRITE_SIZE passes on the same sources)", "traffic_source": k["traffic_source"], "kernel": k["kernel"],
-            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"],
-            "dominant_by": "kernel time in the timed steps",
-            "recipe": "achieved = algorithmic_bytes_per_launch / avg_launch_ms (HIP events, timed region); "
-                      "frac = achieved / peak"}
     if on_chip:
-        roof["note"] = ("dominant kernel reads its scene from LDS: achieved = measured HBM bytes / launch time; "
-                        "its LDS view is under roofline_kernels.k_trace.lds_view")
-        roof["recipe"] = "achieved = PMC HBM bytes per launch / avg_launch_ms; frac = achieved / peak"
+        roof = dict(bound="lds/issue", achieved=k["algorithmic_GBs"], peak=LDS_B128_PEAK_GBS, unit="GB/s",
+                    frac=k["lds_view"]["frac"])
+        if "issue_view" in k:
+            roof["issue_share"] = k["issue_view"].get("active_inst_any_share")
+            roof["wait_share"] = k["issue_view"].get("wait_any_share")
+        other = ks.get("k_shade")
+        if other is not None:
+            roof["hbm_view"] = dict(other["hbm_view"], kernel=other["kernel"],
+                                    note="the shading kernel (path state in HBM) against the HBM peak")
+        roof["note"] = ("dominant kernel reads its SURVEY 8(d) bytes from LDS (scene staged per block): set against "
+                        "the ds_read_b128 aggregate; it is bound by instruction issue and LDS latency "
+                        "(issue_share / wait_share: SQ_ACTIVE_INST_ANY / SQ_WAIT_ANY per wave cycle)")
+    else:
+        roof = dict(bound="hbm", achieved=k["algorithmic_GBs"], peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(k["algorithmic_GBs"] / HBM_PEAK_GBS, 5))
+    roof.update({"traffic": k["hbm_traffic_per_launch"],
+                 "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes on the same sources)",
+                 "traffic_source": k["traffic_source"], "kernel": k["kernel"],
+                 "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"], "avg_launch_ms": k["avg_launch_ms"],
+                 "per_frame_ms": k["per_frame_ms"],
+                 "dominant_by": "kernel time per frame in the isolated frame (one pipeline: launch spans are kernel "
+                                "durations)",
+                 "recipe": "achieved = algorithmic_bytes_per_launch / avg_launch_ms (HIP events on the launch stream, "
+                           "isolated frame; = rocprofv3 --stats average at PT_PIPES=1); frac = achieved / peak"})
+    if ms_per_step is not None:
+        roof["ms_per_step"] = ms_per_step
+        roof["within_step"] = k["per_frame_ms"] <= 1.05 * ms_per_step
+        if not roof["within_step"]:
+            raise RooflineBoundError(f"{k['kernel']}: {k['per_frame_ms']} ms per frame > step {ms_per_step} ms")
     return {"roofline": roof, "roofline_kernels": ks}
 
 
@@ -488,7 +522,8 @@ def main():
         }
         src = source_hash()
         out["source_hash"] = src
-        out.update(rooflines(agg, iso, workload, args.config, lds_scene, names, src))
+        out.update(rooflines(agg, iso, workload, args.config, lds_scene, names, src,
+                             ms_per_step=round(dt / args.steps * 1e3, 2)))
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds, hs)
             if not args.no_parity:

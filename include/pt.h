@@ -287,8 +287,10 @@ typedef struct pt_stats {
     uint64_t trace_launches;
     double shade_ms;           /* summed duration of the shading kernel */
     uint64_t shade_launches;
-    uint64_t shade_bytes;      /* path integrator: algorithmic path-state bytes the shading kernel moved
-                                  (0 unless pt_set_count_bytes is on) */
+    uint64_t shade_bytes;      /* algorithmic path-state bytes the shading kernel moved: path / mypath
+                                  integrators only with pt_set_count_bytes on (0 otherwise); the
+                                  hero_path / hero_path_mis shading kernels always count (a 2-wave
+                                  build either way: the counter register costs them no occupancy) */
     double reduce_ms;          /* pt_render_frame_dist: the ncclReduce of the film (HIP events on the stream) */
 } pt_stats;
 
@@ -407,7 +409,8 @@ pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
 pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
 /* Count the shading kernel's algorithmic path-state bytes (pt_stats.shade_bytes)
  * in the renders that follow (default off: the count costs the 3-waves-per-SIMD
- * shading build a register, so it runs a separate instantiation). */
+ * shading build a register, so it runs a separate instantiation).  Applies to
+ * the path / mypath integrators; the hero integrators always count. */
 pt_status pt_set_count_bytes(pt_scene* scene, int32_t on);
 
 /* Read back a setting of a device scene (what the environment overrides and

@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
+                    base = __builtin_amdgcn_readlane(base, 0);  // the lane that did the atomic, whatever EXEC holds: in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_NB_ATTR void k_trace_nb(DevSc
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
+                    base = __builtin_amdgcn_readlane(base, 0);  // the lane that did the atomic, whatever EXEC holds: in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -767,7 +767,53 @@ __device__ __forceinline__ int lds_top(uint32_t sp) {
     return t;
 }
 
-template <bool kSph>
+// ---- k_trace_lds<kSph, true>: the node step with its lane predicates as VGPR masks ----
+// The node step's control (hit, interior, near side, empty stack, pop) used to
+// be lane masks in SGPRs combined by SALU instructions, plus an exec-mask
+// branch around each step: about 15 SALU per node step, and the CU's one
+// scalar unit (shared by its four SIMDs) was the kernel's busiest pipe
+// (r4_c2_sq_counters.json: 164 K SALU against 294 K VALU per wave).  Here each
+// predicate is a 0 / -1 word in a VGPR (vmask: a v_cndmask, then opaque to the
+// compiler so it is not folded back into a lane mask) and the step's updates
+// are bitwise selects (v_bfi_b32): every lane runs every step, lanes out of
+// node mode with all predicates 0, so nothing changes for them.
+__device__ __forceinline__ int vmask(bool c) {
+    int m = c ? -1 : 0;
+    asm volatile("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ uint32_t vsel(int m, uint32_t a, uint32_t b) {  // m ? a : b for m in {0, -1}
+    return (a & (uint32_t)m) | (b & ~(uint32_t)m);
+}
+// The box test of box_hit_mm as ONE comparison, for rays with tMax > the
+// smallest positive float (denormals are kept: .amdhsa_float_denorm_mode_32 3):
+//   f0 < tMax  <=>  f0 <= pred(tMax)          (pm = pred(tMax), per ray)
+//   f1 > 0     <=>  denorm_min <= f1
+// so max(f0, denorm_min) <= min(f1, pm) is box_hit_mm's !(f0 > f1) & (f0 <
+// tMax) & (f1 > 0), the extra pair denorm_min <= pm holding for such rays.  A
+// NaN x-slab distance fails the reference's test (box_hit_mm's unordered
+// check): v_maximum / v_minimum (IEEE 754-2019, NaN-propagating; gfx950) take
+// tx0 / tx1, so a NaN there makes the comparison false; NaN y / z distances are
+// skipped by v_max3 / v_min3 as in box_hit_mm.
+__device__ __forceinline__ bool box_hit_one(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2,
+                                            float pm) {
+    const float kx = 1 + 2 * gammaf(3);
+    const float tx0 = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
+    float tx1 = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
+    const float ty0 = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
+    float ty1 = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
+    const float tz0 = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
+    float tz1 = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
+    tx1 *= kx;
+    ty1 *= kx;
+    tz1 *= kx;
+    const float dmin = __uint_as_float(1u);
+    const float f0 = __builtin_elementwise_maximum(tx0, __builtin_fmaxf(__builtin_fmaxf(ty0, tz0), dmin));
+    const float f1 = __builtin_elementwise_minimum(tx1, __builtin_fminf(__builtin_fminf(ty1, tz1), pm));
+    return f0 <= f1;
+}
+
+template <bool kSph, bool kVm>
 __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(DevScene sc, DevPaths ps,
                                                                            const uint32_t* __restrict__ rq,
                                                                            const uint32_t* __restrict__ rq_count,
@@ -785,7 +831,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             const uint32_t npax = __float_as_uint(v.w);
             const uint32_t np = npax & 0xffffu;
             const uint32_t off = (uint32_t)__float_as_int(v.z);
-            v.w = __uint_as_float(np ? off + np : 0x80000000u | (1u << (16 + (npax >> 16))));
+            // kVm: the split axis itself in the low bits (v_bfe_i32 of the ray's sign bits at it)
+            v.w = __uint_as_float(np ? off + np : 0x80000000u | (kVm ? (npax >> 16) : (1u << (16 + (npax >> 16)))));
             if (!np) v.z = __uint_as_float(node0 + 32u * off);  // second child: its LDS address
         }
         lds_dyn[i] = v;
@@ -817,7 +864,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
+                    base = __builtin_amdgcn_readlane(base, 0);  // the lane that did the atomic, whatever EXEC holds: in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;
@@ -835,7 +882,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                     inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                     sh = tri_shear(ray.d);
                     n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
-                    sgn = (n0 ? 1u << 16 : 0u) | (n1 ? 1u << 17 : 0u) | (n2 ? 1u << 18 : 0u);
+                    if (kVm) sgn = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
+                    else sgn = (n0 ? 1u << 16 : 0u) | (n1 ? 1u << 17 : 0u) | (n2 ? 1u << 18 : 0u);
                     cur = node0; sp = sbase; hitPrim = -1; leafPos = 0; leafEnd = 0;
                     active = sc.n_nodes > 0;  // empty scene: every ray misses
                     if (!active) {
@@ -895,6 +943,37 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             // steps -- left node mode without a leaf -- instead of being merged after every step
             const bool nm0 = active & (leafPos >= leafEnd);  // done is false here
             bool nm = nm0;
+            // kVm: the VGPR-mask steps, unless a lane in node mode has tMax <= denorm_min (or NaN), where
+            // box_hit_one does not apply (wave-uniform, once per iteration; tMax only shrinks in leaf steps)
+            const float dmin = __uint_as_float(1u);
+            if (kVm && __ballot(nm0 & !(ray.tmax > dmin)) == 0) {
+                const float pm = __uint_as_float(__float_as_uint(ray.tmax) - 1u);  // pred(tMax), tMax > 0
+                int NM = vmask(nm0);
+#pragma unroll
+                for (int u = 0; u < kNodeSteps; ++u) {
+                    nodes -= (uint32_t)NM;  // +1 for lanes in node mode
+                    float4 a, b;
+                    int top;
+                    lds_node_top(cur, sp, &a, &b, &top);  // lanes out of node mode read node0 / their own column
+                    const int H = vmask(box_hit_one(a, b, ray, inv, n0, n1, n2, pm)) & NM;
+                    const uint32_t off = __float_as_uint(b.z);  // leaf: primitivesOffset; interior: second child
+                    const uint32_t w = __float_as_uint(b.w);
+                    const int I = (int)w >> 31;                             // interior node
+                    const int negm = __builtin_amdgcn_sbfe((int)sgn, (int)w, 1);  // the ray runs against its axis
+                    const int inner = H & I;
+                    const int leaf = H & ~I;
+                    const uint32_t c1 = cur + 32u;
+                    lds_push(sp, (int)vsel(negm, c1, off));  // the far child (kept only for an interior node)
+                    const int E = ((int)(sp - sbase) - 1) >> 31;  // empty stack
+                    const int pop = NM & ~H & ~E;
+                    cur = vsel(inner, vsel(negm, off, c1), vsel(pop, (uint32_t)top, node0));
+                    sp += (uint32_t)(inner & 512) - (uint32_t)(pop & 512);
+                    leafPos = (int)vsel(leaf, off, (uint32_t)leafPos);
+                    leafEnd = (int)vsel(leaf, w, (uint32_t)leafEnd);
+                    NM = inner | pop;
+                }
+                nm = NM != 0;
+            } else {
 #pragma unroll
             for (int u = 0; u < kNodeSteps; ++u) {
                 if (!nm) continue;
@@ -907,7 +986,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 const uint32_t w = __float_as_uint(b.w);
                 const bool inner = hit & ((int)w < 0);
                 const bool leaf = hit & ((int)w >= 0);
-                const bool neg = (w & sgn) != 0;
+                const bool neg = kVm ? ((sgn >> (w & 31u)) & 1u) != 0 : (w & sgn) != 0;
                 const bool empty = sp == sbase;
                 lds_push(sp, (int)(neg ? cur + 32u : off));  // the far child (kept only for an interior node)
                 const bool pop = !hit & !empty;
@@ -916,6 +995,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 sp = inner ? sp + 512 : (pop ? sp - 512 : sp);
                 leafPos = leaf ? (int)off : leafPos;
                 leafEnd = leaf ? (int)w : leafEnd;
+            }
             }
             done = nm0 & !nm & (leafPos >= leafEnd);  // the ray left the BVH: stack empty on a miss
         }
@@ -1037,7 +1117,7 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
                 if (qn >= qe && !drained) {
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
-                    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 (the wave is whole here): uniform, in an SGPR
+                    base = __builtin_amdgcn_readlane(base, 0);  // the lane that did the atomic, whatever EXEC holds: in an SGPR
                     qn = base < n ? base : n;
                     qe = base + kTraceChunk < n ? base + kTraceChunk : n;
                     drained = base + kTraceChunk >= n;

@@ -922,8 +922,11 @@ class Loader {
                 // its whole pairs, and only nvi / 3 triangles are made.
                 const Param* pi = ps.find("indices", {"integer"});
                 const Param* pp = ps.find("P", {"point"});
-                const Param* puv = ps.find("uv", {"point2", "float"});
-                if (!puv) puv = ps.find("st", {"point2", "float"});
+                // the reference's lookup order: point2 uv, point2 st, then float uv, float st
+                const Param* puv = ps.find("uv", {"point2"});
+                if (!puv) puv = ps.find("st", {"point2"});
+                if (!puv) puv = ps.find("uv", {"float"});
+                if (!puv) puv = ps.find("st", {"float"});
                 const int nv = pp ? (int)(pp->nums.size() / 3) : 0;
                 const int nuv = puv ? (int)(puv->nums.size() / 2) : 0;
                 bool useUV = puv != nullptr && nuv > 0;

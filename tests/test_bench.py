@@ -43,32 +43,59 @@ def _timed(trace_ms, shade_ms):
             "node_visits": 10 ** 9, "prim_tests": 10 ** 8, "shade_bytes": 10 ** 12}
 
 
-def test_roofline_kernel_is_timed_dominant_and_traffic_needs_same_sources(tmp_path, monkeypatch):
-    """The roofline names the kernel with the most time in the TIMED steps
-    (not in the isolated frame), and a PMC summary taken on other sources is
-    reported as stale, never used as `traffic`."""
+def test_roofline_kernel_is_isolated_dominant_and_traffic_needs_same_sources(tmp_path, monkeypatch):
+    """The roofline names the kernel with the most time per frame in the
+    ISOLATED frame (one pipeline: launch spans are kernel durations), not in
+    the timed steps, where two pipelines overlap and a launch's span includes
+    the co-running kernel (kept only as overlapped_span_ms); achieved / frac
+    come from the isolated launch time.  A PMC summary taken on other sources
+    is reported as stale, never used as `traffic`."""
     os.makedirs(tmp_path / "profiles")
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     wl = "w"
     pmc = {"workload": wl, "source_hash": "old", "kernels": {
-        "void pt::k_shade_w3<16>": {"launches": 10, "hbm_bytes_per_launch": 2.0e10}}}
+        "void pt::k_shade_w3<16>": {"launches": 10, "hbm_bytes_per_launch": 2.0e10},
+        "void pt::k_trace_pt<false, true, false>": {"launches": 10, "hbm_bytes_per_launch": 3.0e10}}}
     (tmp_path / "profiles" / "r3_pmc_traffic.json").write_text(json.dumps(pmc))
-    timed = dict(_timed(400.0, 500.0), shade_bytes=0)  # shading dominates the timed region (bytes not counted there)
-    iso = _timed(350.0, 270.0)            # ... though tracing dominates the isolated frame, which counts the bytes
-    out = bench.rooflines(timed, iso, wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new")
+    timed = dict(_timed(400.0, 500.0), shade_bytes=0)  # shading dominates the overlapped timed spans ...
+    iso = _timed(350.0, 270.0)            # ... tracing dominates the isolated frame
+    # LDS-resident traversal dominant: bound lds/issue, the shading kernel's HBM fraction beside it
+    out = bench.rooflines(timed, iso, wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new", ms_per_step=600.0)
     roof = out["roofline"]
-    assert roof["kernel"] == "k_shade_w3"
-    assert roof["avg_launch_ms"] == 5.0
-    assert roof["achieved"] == round(1e10 / 5e-3 / 1e9, 1) and roof["frac"] == round(roof["achieved"] / 8000.0, 5)
+    assert roof["kernel"] == "k_trace_lds" and roof["bound"] == "lds/issue"
+    assert roof["avg_launch_ms"] == 3.5 and roof["per_frame_ms"] == 350.0 and roof["within_step"]
+    alg = (32.0 * 10 ** 9 + 48.0 * 10 ** 8) / 100
+    assert roof["achieved"] == round(alg / 3.5e-3 / 1e9, 1) and roof["peak"] == 150000.0
+    assert roof["frac"] == round(roof["achieved"] / 150000.0, 5)
+    assert roof["hbm_view"]["kernel"] == "k_shade_w3"
+    assert roof["hbm_view"]["frac"] == round(round(1e10 / 2.7e-3 / 1e9, 1) / 8000.0, 5)
+    assert out["roofline_kernels"]["k_shade"]["overlapped_span_ms"] == 5.0
     assert roof["traffic"] is None
     assert "other sources" in out["roofline_kernels"]["k_shade"]["traffic_stale"]
-    lv = out["roofline_kernels"]["k_trace"]["lds_view"]
-    assert lv["peak"] == 150000.0
+    # HBM-resident traversal dominant (C5): bound hbm from the isolated launch time
+    out = bench.rooflines(timed, iso, wl, "c5", False, ("k_trace_pt", "k_shade"), "new")
+    roof = out["roofline"]
+    assert roof["kernel"] == "k_trace_pt" and roof["bound"] == "hbm"
+    assert roof["frac"] == round(round(alg / 3.5e-3 / 1e9, 1) / 8000.0, 5)
+    # shading dominant in the isolated frame
+    out = bench.rooflines(timed, _timed(200.0, 270.0), wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new")
+    assert out["roofline"]["kernel"] == "k_shade_w3" and out["roofline"]["bound"] == "hbm"
+    assert out["roofline"]["achieved"] == round(1e10 / 2.7e-3 / 1e9, 1)
     pmc["source_hash"] = "new"
     (tmp_path / "profiles" / "r4_pmc_traffic.json").write_text(json.dumps(pmc))
-    out = bench.rooflines(timed, iso, wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new")
+    out = bench.rooflines(timed, _timed(200.0, 270.0), wl, "c2", True, ("k_trace_lds", "k_shade_w3"), "new")
     assert out["roofline"]["traffic"] == 2.0e10
     assert out["roofline"]["traffic_source"].endswith("r4_pmc_traffic.json")
+
+
+def test_roofline_bound_check():
+    """The dominant kernel's isolated time per frame may not exceed the step
+    (round 4's line set a 632-ms overlapped span against a 597-ms step)."""
+    timed, iso = _timed(400.0, 500.0), _timed(350.0, 270.0)
+    ok = bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_lds", "k_shade_w3"), "x", ms_per_step=340.0)
+    assert ok["roofline"]["within_step"]  # 350 <= 1.05 * 340
+    with pytest.raises(bench.RooflineBoundError):
+        bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_lds", "k_shade_w3"), "x", ms_per_step=300.0)
 
 
 @pytest.mark.gpu

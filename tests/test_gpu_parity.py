@@ -121,6 +121,7 @@ def _edge_rays(sc, n_rand, n_edge, seed, tmax):
 
 TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
     "k_trace_lds": {},
+    "k_trace_lds_lanemask": {"PT_TRACE_VM": "0"},
     "k_trace_oct": {"PT_TRACE_OCT": "1"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
@@ -140,6 +141,34 @@ def test_frame_traversal_kernels_bit_exact(variant, monkeypatch, kernel, any_hit
         monkeypatch.setenv(k, v)
     hs, sc = _scene(variant(**MINI))
     rays = _edge_rays(sc, 6000, 6000, 5, np.inf if not any_hit else 300.0)
+    _, order = sc.bvh()
+    got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
+    ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
+    if not any_hit:
+        got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
+    assert np.array_equal(got, ref)
+    assert (nodes, prims) == (rnodes, rprims)
+
+
+@pytest.mark.parametrize("kernel", ["k_trace_lds", "k_trace_lds_lanemask"])
+@pytest.mark.parametrize("any_hit", [False, True])
+def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel, any_hit):
+    """k_trace_lds's one-comparison box test holds for tMax > the smallest
+    denormal; rays at or below it (0, +-denormals, the denormal range, NaN)
+    take the lane-mask steps.  Rays with such tMax values mixed into every
+    wave, and tMax values just around box distances: hits and node /
+    primitive counters equal the oracle's (Bounds3::IntersectP,
+    geometry.h:1584-1606, tMin < ray.tMax && tMax > 0)."""
+    for k, v in TRACE_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+    hs, sc = _scene(variant(**MINI))
+    rays = _edge_rays(sc, 4000, 4000, 11, np.inf)
+    rng = np.random.default_rng(12)
+    tiny = np.array([0.0, -0.0, 1e-45, 3e-45, 1e-40, 1.17549435e-38, 1e-30, np.nan, -1.0], np.float32)
+    pick = rng.random(len(rays))
+    tm = np.where(pick < 0.15, tiny[rng.integers(len(tiny), size=len(rays))],
+                  np.where(pick < 0.6, rng.uniform(0, 20, len(rays)).astype(np.float32), np.float32(np.inf)))
+    rays[:, 6] = tm.astype(np.float32)
     _, order = sc.bvh()
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
@@ -774,6 +803,30 @@ def test_full_config_sparse_tiles_bit_exact():
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
         assert gst[k] == rst[k], k
+
+
+@pytest.mark.parametrize("equal", ["1", "2"])
+def test_batch_equal_two_pipelines_bit_exact(tmp_path, monkeypatch, equal):
+    """PT_BATCH_EQUAL splits a render into equal batches (rounded to whole
+    16x16 tiles: the FilmTile boundaries the ordered film merge depends on)
+    run by two pipelines: a full render and a rank's tile shard
+    (render_accum(rank, nranks)) give the oracle's film bit for bit."""
+    from conftest import scene_variant
+    monkeypatch.setenv("PT_BATCH_EQUAL", equal)
+    monkeypatch.setenv("PT_PIPES", "2")
+    path = scene_variant(tmp_path, name="portal_cornell.pbrt", res=(120, 72), spp=8)
+    hs = ptgpu.HostScene(path)
+    sc = ptgpu.Scene(hs, batch_slots=16 * 16 * 8 * 7)  # several batches per render
+    assert sc.query("pipelines") == 2
+    got, gst = sc.render_accum(0, 1)
+    ref, rst = pyoracle.render_accum(hs.desc, nthreads=8)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for r in range(3):
+        got, gst = sc.render_accum(r, 3)
+        ref, rst = pyoracle.render_accum(hs.desc, nthreads=8, tile_offset=r, tile_stride=3)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        for k in ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+            assert gst[k] == rst[k], k
 
 
 def test_count_bytes_build_renders_the_same(variant):

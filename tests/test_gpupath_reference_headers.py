@@ -1,0 +1,117 @@
+"""The reference-side binding (integration/gpupath.cpp) against the
+reference's OWN headers, not the stub mirror: the headers of
+/root/reference/src are copied to a temporary directory, the INTEGRATION.md §1
+accessor patch is applied to the copy (integration/accessor_patch.py), and
+g++ -fsyntax-only checks gpupath.cpp against it.  A member renamed or retyped
+in the reference (LinearBVHNode, AAPortal::portal, PortalArealight::portals,
+AAPlaneShape's lo / hi / ax, the material and light members the accessors
+return) fails this test.
+
+This is a syntax check of this repo's binding, not a build of the reference:
+no reference source is compiled to code and nothing runs.  The reference's
+headers include <glog/logging.h>, whose git submodule is empty here, so the
+test writes a header declaring the logging macros they use (CHECK*, DCHECK*,
+LOG, VLOG) as no-op streams; nothing else is substituted.  Skipped where
+/root/reference is absent (the GPU box)."""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_SRC = "/root/reference/src"
+sys.path.insert(0, os.path.join(REPO, "integration"))
+import accessor_patch  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources not present")
+
+GLOG_MACROS = """#pragma once
+// test-only: the logging macros the reference headers use, as no-op streams
+struct PtNullLogStream {
+    template <class T> PtNullLogStream &operator<<(const T &) { return *this; }
+};
+#define PT_NULL_LOG PtNullLogStream()
+#define CHECK(c) PT_NULL_LOG
+#define CHECK_EQ(a, b) PT_NULL_LOG
+#define CHECK_NE(a, b) PT_NULL_LOG
+#define CHECK_LT(a, b) PT_NULL_LOG
+#define CHECK_LE(a, b) PT_NULL_LOG
+#define CHECK_GT(a, b) PT_NULL_LOG
+#define CHECK_GE(a, b) PT_NULL_LOG
+#define CHECK_NOTNULL(p) (p)
+#define DCHECK(c) PT_NULL_LOG
+#define DCHECK_EQ(a, b) PT_NULL_LOG
+#define DCHECK_NE(a, b) PT_NULL_LOG
+#define DCHECK_LT(a, b) PT_NULL_LOG
+#define DCHECK_LE(a, b) PT_NULL_LOG
+#define DCHECK_GT(a, b) PT_NULL_LOG
+#define DCHECK_GE(a, b) PT_NULL_LOG
+#define LOG(s) PT_NULL_LOG
+#define VLOG(n) PT_NULL_LOG
+"""
+
+
+# The compile definitions the reference's CMakeLists.txt sets for a Linux g++ build
+# (CMakeLists.txt:109-285: the feature probes' results for this toolchain)
+REF_DEFINES = ["-DPBRT_HAVE_ALLOCA_H", "-DPBRT_HAVE_MEMORY_H", "-DPBRT_HAVE_HEX_FP_CONSTANTS",
+               "-DPBRT_HAVE_BINARY_CONSTANTS", "-DPBRT_HAVE_CONSTEXPR", "-DPBRT_CONSTEXPR=constexpr",
+               "-DPBRT_HAVE_ALIGNAS", "-DPBRT_HAVE_ALIGNOF", "-DPBRT_HAVE_ITIMER", "-DPBRT_HAVE_NONPOD_IN_UNIONS",
+               "-DPBRT_HAVE_MMAP", "-DPBRT_HAVE_POSIX_MEMALIGN", "-DPBRT_THREAD_LOCAL=thread_local"]
+
+
+def _patched_headers(tmp_path):
+    src = tmp_path / "src"
+    for root, dirs, files in os.walk(REF_SRC):
+        dirs[:] = [d for d in dirs if d != "ext"]
+        for f in files:
+            if f.endswith(".h"):
+                rel = os.path.relpath(os.path.join(root, f), REF_SRC)
+                os.makedirs(src / os.path.dirname(rel), exist_ok=True)
+                shutil.copyfile(os.path.join(root, f), src / rel)
+    accessor_patch.apply(str(src))
+    os.makedirs(tmp_path / "logstub" / "glog")
+    (tmp_path / "logstub" / "glog" / "logging.h").write_text(GLOG_MACROS)
+    return src
+
+
+def test_binding_compiles_against_reference_headers(tmp_path):
+    src = _patched_headers(tmp_path)
+    r = subprocess.run(["g++", "-std=gnu++11", "-fsyntax-only"] + REF_DEFINES + ["-I", str(src), "-I", str(src / "core"), "-I", str(tmp_path / "logstub"),
+                        "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "integration"),
+                        os.path.join(REPO, "integration", "gpupath.cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+def test_patch_leaves_reference_untouched_and_is_needed(tmp_path):
+    """Without the accessor patch the binding does NOT compile (the getters
+    are the patch's, not the reference's), and the patch wrote only to the
+    copy."""
+    src = tmp_path / "plain"
+    shutil.copytree(REF_SRC, src, ignore=shutil.ignore_patterns("ext", "*.cpp", "*.c"))
+    os.makedirs(tmp_path / "logstub" / "glog")
+    (tmp_path / "logstub" / "glog" / "logging.h").write_text(GLOG_MACROS)
+    r = subprocess.run(["g++", "-std=gnu++11", "-fsyntax-only"] + REF_DEFINES + ["-I", str(src), "-I", str(src / "core"),
+                        "-I", str(tmp_path / "logstub"), "-I", os.path.join(REPO, "include"),
+                        os.path.join(REPO, "integration", "gpupath.cpp")], capture_output=True, text=True)
+    assert r.returncode != 0 and "GetAggregate" in r.stderr
+    assert "PATCH" not in open(os.path.join(REF_SRC, "core", "scene.h")).read()
+
+
+def test_stub_mirror_declares_the_patch_accessors():
+    """The stub headers the CPU / GPU binding tests compile against
+    (integration/pbrt_stub/stub_pbrt.h) declare exactly the accessors the
+    patch adds, class by class."""
+    stub = open(os.path.join(REPO, "integration", "pbrt_stub", "stub_pbrt.h")).read()
+    for cls, names in accessor_patch.getter_names().items():
+        m = re.search(r"\b(class|struct)\s+%s\b[^;{]*\{" % cls, stub)
+        assert m, cls
+        depth, i = 1, m.end()
+        while depth:
+            depth += (stub[i] == "{") - (stub[i] == "}")
+            i += 1
+        body = stub[m.end():i]
+        declared = set(re.findall(r"(\w+)\(\) const \{", body))
+        assert set(names) <= declared, (cls, set(names) - declared)

@@ -152,6 +152,21 @@ def test_trianglemesh_error_contract(tmp_path, shape, ntris):
     assert np.isfinite(img).all() and st["samples"] == 8 * 8 * 4
 
 
+@pytest.mark.parametrize("uvs,has_uv", [
+    ('"float uv" [0 0 1 0] "point2 st" [0 0 1 0 0 1]', True),   # point2 st before float uv: st is used
+    ('"point2 uv" [0 0 1 0] "float st" [0 0 1 0 0 1]', False),  # point2 uv (too few: discarded) wins
+    ('"float st" [0 0 1 0 0 1] "float uv" [0 0 1 0]', False),   # float uv before float st
+])
+def test_trianglemesh_uv_lookup_order(tmp_path, uvs, has_uv):
+    """CreateTriangleMeshShape looks the uv array up as point2 "uv", point2
+    "st", float "uv", float "st" (triangle.cpp:918-923): the first found is
+    used (and discarded when shorter than P), later ones are not consulted."""
+    hs = ptgpu.HostScene(_mesh_scene(tmp_path, 'Shape "trianglemesh" ' + TRI + ' "integer indices" [0 1 2] ' + uvs))
+    d = ptgpu.scene_desc(hs)
+    words = ctypes.cast(d.triangles, ctypes.POINTER(ctypes.c_uint32))
+    assert bool(words[12 * 6 + 5] & 8) == has_uv  # PT_TRI_HAS_UV
+
+
 def test_empty_emitter_mesh_adds_no_light(tmp_path):
     """An empty trianglemesh under an AreaLightSource (spotlight/test00001.pbrt)
     leaves the scene exactly as if the attribute block were absent: same
