@@ -767,53 +767,7 @@ __device__ __forceinline__ int lds_top(uint32_t sp) {
     return t;
 }
 
-// ---- k_trace_lds<kSph, true>: the node step with its lane predicates as VGPR masks ----
-// The node step's control (hit, interior, near side, empty stack, pop) used to
-// be lane masks in SGPRs combined by SALU instructions, plus an exec-mask
-// branch around each step: about 15 SALU per node step, and the CU's one
-// scalar unit (shared by its four SIMDs) was the kernel's busiest pipe
-// (r4_c2_sq_counters.json: 164 K SALU against 294 K VALU per wave).  Here each
-// predicate is a 0 / -1 word in a VGPR (vmask: a v_cndmask, then opaque to the
-// compiler so it is not folded back into a lane mask) and the step's updates
-// are bitwise selects (v_bfi_b32): every lane runs every step, lanes out of
-// node mode with all predicates 0, so nothing changes for them.
-__device__ __forceinline__ int vmask(bool c) {
-    int m = c ? -1 : 0;
-    asm volatile("" : "+v"(m));
-    return m;
-}
-__device__ __forceinline__ uint32_t vsel(int m, uint32_t a, uint32_t b) {  // m ? a : b for m in {0, -1}
-    return (a & (uint32_t)m) | (b & ~(uint32_t)m);
-}
-// The box test of box_hit_mm as ONE comparison, for rays with tMax > the
-// smallest positive float (denormals are kept: .amdhsa_float_denorm_mode_32 3):
-//   f0 < tMax  <=>  f0 <= pred(tMax)          (pm = pred(tMax), per ray)
-//   f1 > 0     <=>  denorm_min <= f1
-// so max(f0, denorm_min) <= min(f1, pm) is box_hit_mm's !(f0 > f1) & (f0 <
-// tMax) & (f1 > 0), the extra pair denorm_min <= pm holding for such rays.  A
-// NaN x-slab distance fails the reference's test (box_hit_mm's unordered
-// check): v_maximum / v_minimum (IEEE 754-2019, NaN-propagating; gfx950) take
-// tx0 / tx1, so a NaN there makes the comparison false; NaN y / z distances are
-// skipped by v_max3 / v_min3 as in box_hit_mm.
-__device__ __forceinline__ bool box_hit_one(float4 a, float4 b, const Ray& ray, V3 inv, bool n0, bool n1, bool n2,
-                                            float pm) {
-    const float kx = 1 + 2 * gammaf(3);
-    const float tx0 = ((n0 ? a.w : a.x) - ray.o.x) * inv.x;
-    float tx1 = ((n0 ? a.x : a.w) - ray.o.x) * inv.x;
-    const float ty0 = ((n1 ? b.x : a.y) - ray.o.y) * inv.y;
-    float ty1 = ((n1 ? a.y : b.x) - ray.o.y) * inv.y;
-    const float tz0 = ((n2 ? b.y : a.z) - ray.o.z) * inv.z;
-    float tz1 = ((n2 ? a.z : b.y) - ray.o.z) * inv.z;
-    tx1 *= kx;
-    ty1 *= kx;
-    tz1 *= kx;
-    const float dmin = __uint_as_float(1u);
-    const float f0 = __builtin_elementwise_maximum(tx0, __builtin_fmaxf(__builtin_fmaxf(ty0, tz0), dmin));
-    const float f1 = __builtin_elementwise_minimum(tx1, __builtin_fminf(__builtin_fminf(ty1, tz1), pm));
-    return f0 <= f1;
-}
-
-template <bool kSph, bool kVm>
+template <bool kSph>
 __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(DevScene sc, DevPaths ps,
                                                                            const uint32_t* __restrict__ rq,
                                                                            const uint32_t* __restrict__ rq_count,
@@ -831,8 +785,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             const uint32_t npax = __float_as_uint(v.w);
             const uint32_t np = npax & 0xffffu;
             const uint32_t off = (uint32_t)__float_as_int(v.z);
-            // kVm: the split axis itself in the low bits (v_bfe_i32 of the ray's sign bits at it)
-            v.w = __uint_as_float(np ? off + np : 0x80000000u | (kVm ? (npax >> 16) : (1u << (16 + (npax >> 16)))));
+            v.w = __uint_as_float(np ? off + np : 0x80000000u | (1u << (16 + (npax >> 16))));
             if (!np) v.z = __uint_as_float(node0 + 32u * off);  // second child: its LDS address
         }
         lds_dyn[i] = v;
@@ -882,8 +835,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                     inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                     sh = tri_shear(ray.d);
                     n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
-                    if (kVm) sgn = (n0 ? 1u : 0u) | (n1 ? 2u : 0u) | (n2 ? 4u : 0u);
-                    else sgn = (n0 ? 1u << 16 : 0u) | (n1 ? 1u << 17 : 0u) | (n2 ? 1u << 18 : 0u);
+                    sgn = (n0 ? 1u << 16 : 0u) | (n1 ? 1u << 17 : 0u) | (n2 ? 1u << 18 : 0u);
                     cur = node0; sp = sbase; hitPrim = -1; leafPos = 0; leafEnd = 0;
                     active = sc.n_nodes > 0;  // empty scene: every ray misses
                     if (!active) {
@@ -943,37 +895,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
             // steps -- left node mode without a leaf -- instead of being merged after every step
             const bool nm0 = active & (leafPos >= leafEnd);  // done is false here
             bool nm = nm0;
-            // kVm: the VGPR-mask steps, unless a lane in node mode has tMax <= denorm_min (or NaN), where
-            // box_hit_one does not apply (wave-uniform, once per iteration; tMax only shrinks in leaf steps)
-            const float dmin = __uint_as_float(1u);
-            if (kVm && __ballot(nm0 & !(ray.tmax > dmin)) == 0) {
-                const float pm = __uint_as_float(__float_as_uint(ray.tmax) - 1u);  // pred(tMax), tMax > 0
-                int NM = vmask(nm0);
-#pragma unroll
-                for (int u = 0; u < kNodeSteps; ++u) {
-                    nodes -= (uint32_t)NM;  // +1 for lanes in node mode
-                    float4 a, b;
-                    int top;
-                    lds_node_top(cur, sp, &a, &b, &top);  // lanes out of node mode read node0 / their own column
-                    const int H = vmask(box_hit_one(a, b, ray, inv, n0, n1, n2, pm)) & NM;
-                    const uint32_t off = __float_as_uint(b.z);  // leaf: primitivesOffset; interior: second child
-                    const uint32_t w = __float_as_uint(b.w);
-                    const int I = (int)w >> 31;                             // interior node
-                    const int negm = __builtin_amdgcn_sbfe((int)sgn, (int)w, 1);  // the ray runs against its axis
-                    const int inner = H & I;
-                    const int leaf = H & ~I;
-                    const uint32_t c1 = cur + 32u;
-                    lds_push(sp, (int)vsel(negm, c1, off));  // the far child (kept only for an interior node)
-                    const int E = ((int)(sp - sbase) - 1) >> 31;  // empty stack
-                    const int pop = NM & ~H & ~E;
-                    cur = vsel(inner, vsel(negm, off, c1), vsel(pop, (uint32_t)top, node0));
-                    sp += (uint32_t)(inner & 512) - (uint32_t)(pop & 512);
-                    leafPos = (int)vsel(leaf, off, (uint32_t)leafPos);
-                    leafEnd = (int)vsel(leaf, w, (uint32_t)leafEnd);
-                    NM = inner | pop;
-                }
-                nm = NM != 0;
-            } else {
 #pragma unroll
             for (int u = 0; u < kNodeSteps; ++u) {
                 if (!nm) continue;
@@ -986,7 +907,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 const uint32_t w = __float_as_uint(b.w);
                 const bool inner = hit & ((int)w < 0);
                 const bool leaf = hit & ((int)w >= 0);
-                const bool neg = kVm ? ((sgn >> (w & 31u)) & 1u) != 0 : (w & sgn) != 0;
+                const bool neg = (w & sgn) != 0;
                 const bool empty = sp == sbase;
                 lds_push(sp, (int)(neg ? cur + 32u : off));  // the far child (kept only for an interior node)
                 const bool pop = !hit & !empty;
@@ -995,7 +916,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_LDS_ATTR void k_trace_lds(Dev
                 sp = inner ? sp + 512 : (pop ? sp - 512 : sp);
                 leafPos = leaf ? (int)off : leafPos;
                 leafEnd = leaf ? (int)w : leafEnd;
-            }
             }
             done = nm0 & !nm & (leafPos >= leafEnd);  // the ray left the BVH: stack empty on a miss
         }
@@ -1658,11 +1578,13 @@ __device__ __forceinline__ void path_load_now(const DevScene& sc, const DevPaths
 // Two stages: the head record (state word with the payload flags, hits) two
 // paths ahead, the body one path ahead and only what the head says this step
 // will read.
+// kMis: the scene has lights the MIS branch samples -- only then can ray B (its hit word) be pending
+template <bool kMis = true>
 __device__ __forceinline__ void path_prefetch_head(const DevPaths& ps, uint32_t slot, PathPre* p) {
     p->st = *st_word(ps, slot);
     p->hit = *hit_word(ps, slot, kHdHit);
     p->hitA = *hit_word(ps, slot, kHdHitA);
-    p->hitB = *hit_word(ps, slot, kHdHitB);
+    p->hitB = kMis ? *hit_word(ps, slot, kHdHitB) : -1;
 }
 __device__ __forceinline__ void path_prefetch_body(const DevPaths& ps, uint32_t slot, PathPre* p) {
     const float3 a = *reinterpret_cast<const float3*>(body_word(ps, slot, kBdL));
@@ -1908,7 +1830,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
             slot = pq[i];
             PathPre pre{};
             PathNow now{};
-            path_prefetch_head(ps, slot, &pre);
+            path_prefetch_head<Ft<kFt>::mis>(ps, slot, &pre);
             path_prefetch_body(ps, slot, &pre);
             path_load_now<kFt>(sc, ps, slot, pre, &now);
             shade_path<kFt>(sc, hl, ps, slot, pre, now, &rays, &keep, &overflow, PT_ABP);
@@ -1922,7 +1844,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         PathPre pre{};  // this path's head (its body is loaded when its step starts)
         if (i0 < n) {
             slot = pq[i0];
-            path_prefetch_head(ps, slot, &pre);
+            path_prefetch_head<Ft<kFt>::mis>(ps, slot, &pre);
         }
         if (i0 + stride < n) slot1 = pq[i0 + stride];
         for (; base < n; base += stride) {
@@ -1934,7 +1856,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
                 path_prefetch_body(ps, slot, &pre);
                 path_load_now<kFt>(sc, ps, slot, pre, &now);
             }
-            if (i + stride < n) path_prefetch_head(ps, slot1, &nxt);
+            if (i + stride < n) path_prefetch_head<Ft<kFt>::mis>(ps, slot1, &nxt);
             if (i + 2 * stride < n) slot2 = pq[i + 2 * stride];
             RayList rays;
             bool keep = false;
@@ -1950,12 +1872,12 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
     PathPre pre{}, nxt{};  // this path (complete) and the next one (head only)
     if (i0 < n) {
         slot = pq[i0];
-        path_prefetch_head(ps, slot, &pre);
+        path_prefetch_head<Ft<kFt>::mis>(ps, slot, &pre);
         path_prefetch_body(ps, slot, &pre);
     }
     if (i0 + stride < n) {
         slot1 = pq[i0 + stride];
-        path_prefetch_head(ps, slot1, &nxt);
+        path_prefetch_head<Ft<kFt>::mis>(ps, slot1, &nxt);
     }
     if (i0 + 2 * stride < n) slot2 = pq[i0 + 2 * stride];
     for (; base < n; base += stride) {
@@ -1965,7 +1887,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         uint32_t slot3 = 0;
         if (i < n) path_load_now<kFt>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
         if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
-        if (i + 2 * stride < n) path_prefetch_head(ps, slot2, &nn);
+        if (i + 2 * stride < n) path_prefetch_head<Ft<kFt>::mis>(ps, slot2, &nn);
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
         RayList rays;
         bool keep = false;

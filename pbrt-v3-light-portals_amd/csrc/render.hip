@@ -286,7 +286,6 @@ struct pt_scene {
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
-    bool trace_vm = true;        // k_trace_lds node steps with VGPR-mask predicates (PT_TRACE_VM=0: lane-mask steps)
     size_t oct_lds_bytes = 0;    // > 0: k_trace_oct (octant images of an LDS-sized BVH; opt-in PT_TRACE_OCT=1)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
@@ -402,10 +401,7 @@ static TraceNbKernel trace_nb_kernel(bool lds, bool sph) {
     return lds ? (sph ? k_trace_nb<true, true> : k_trace_nb<true, false>)
                : (sph ? k_trace_nb<false, true> : k_trace_nb<false, false>);
 }
-static TraceNbKernel trace_lds_kernel(bool sph, bool vm) {
-    return vm ? (sph ? k_trace_lds<true, true> : k_trace_lds<false, true>)
-              : (sph ? k_trace_lds<true, false> : k_trace_lds<false, false>);
-}
+static TraceNbKernel trace_lds_kernel(bool sph) { return sph ? k_trace_lds<true> : k_trace_lds<false>; }
 static TraceNbKernel trace_oct_kernel(bool sph) { return sph ? k_trace_oct<true> : k_trace_oct<false>; }
 using TracePtKernel = void (*)(DevScene, DevPaths, const uint32_t*, const uint32_t*, uint32_t*, int, int, int, int*,
                                DevStats*);
@@ -1138,7 +1134,7 @@ static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_
     } else if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
         // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
-        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres, s->trace_vm), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
+        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
                            counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
     } else if (s->trace_persist == 2 && !s->trace_spill) {
         // branch-reduced persistent traversal; LDS stack of depth+1 rows
@@ -1663,7 +1659,6 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     s->has_spheres = (s->features & kFtSphere) != 0;
     if (const char* t = std::getenv("PT_TRACE_PERSIST")) s->trace_persist = std::atoi(t);
     if (const char* t = std::getenv("PT_TRACE_LEAN")) s->trace_lean = t[0] != '0';
-    if (const char* t = std::getenv("PT_TRACE_VM")) s->trace_vm = t[0] != '0';
     {   // k_trace_oct when four blocks of it fit a CU's LDS (160 KB): octant images + primitives + stack
         const size_t oct = 8 * 32 * (size_t)s->dev.n_nodes + 48 * (size_t)s->dev.n_prims +
                            (size_t)(s->stack_rows + 2) * kOctBlock * sizeof(int);

@@ -12,10 +12,8 @@ template __global__ void k_trace_nb<false, false>(PT_ARGS, uint32_t*, int, int, 
 template __global__ void k_trace_nb<false, true>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_nb<true, false>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_nb<true, true>(PT_ARGS, uint32_t*, int, int, DevStats*);
-template __global__ void k_trace_lds<false, false>(PT_ARGS, uint32_t*, int, int, DevStats*);
-template __global__ void k_trace_lds<true, false>(PT_ARGS, uint32_t*, int, int, DevStats*);
-template __global__ void k_trace_lds<false, true>(PT_ARGS, uint32_t*, int, int, DevStats*);
-template __global__ void k_trace_lds<true, true>(PT_ARGS, uint32_t*, int, int, DevStats*);
+template __global__ void k_trace_lds<false>(PT_ARGS, uint32_t*, int, int, DevStats*);
+template __global__ void k_trace_lds<true>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_oct<false>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_oct<true>(PT_ARGS, uint32_t*, int, int, DevStats*);
 #define PT_PT(a, b, c) template __global__ void k_trace_pt<a, b, c>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);

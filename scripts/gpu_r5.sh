@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round-5 evidence on one GPU.  Every GPU step has its own time limit; the
 # script stops at the first failure.
-#   STAGES (default "tests bench prof1 pmc sq"): any subset of tests bench ab prof prof1 pmc sq, run in that order
+#   STAGES (default "tests bench prof1 pmc sq"): any subset of tests bench ab prof prof1 pmc sq calib, run in that order
 #          prof1: kernel-trace --stats with PT_PIPES=1 (one pipeline: every launch runs alone, so the averages
-#          are kernel durations -- what the bench line's roofline uses)
+#          are kernel durations -- what the bench line's roofline uses); calib: tools/fetch_calib with
+#          FETCH_SIZE / WRITE_SIZE passes (scripts/fetch_calib_summary.py)
 #   CFG    bench --config for bench/prof/pmc/sq (default c2); OUT tag (default $CFG)
 #   BARGS  extra bench args for prof/pmc (e.g. "--spp 64")
 # Outputs under gpurun_out/r5_$OUT/: source_hash.txt, pytest_gpu.log, smoke.log,
@@ -74,5 +75,17 @@ if has sq; then
     --output-format csv -- python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline $SQ \
     > "$o/sq2.log" 2>&1
   rc=$?; echo "pmc sq2 rc=$rc"; ok $rc sq2
+fi
+if has calib; then
+  # FETCH_SIZE / WRITE_SIZE calibration: known bytes in the shading kernels' access shapes
+  T="$R/pbrt-v3-light-portals_amd/tools/fetch_calib"
+  timeout -k 10 120 "$T" 3 > "$o/calib.log" 2>&1
+  rc=$?; echo "calib rc=$rc"; ok $rc calib
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d "$o/pmc_cfetch" -o cfetch --output-format csv -- "$T" 1 \
+    > "$o/cfetch.log" 2>&1
+  rc=$?; echo "calib fetch rc=$rc"; ok $rc cfetch
+  timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d "$o/pmc_cwrite" -o cwrite --output-format csv -- "$T" 1 \
+    > "$o/cwrite.log" 2>&1
+  rc=$?; echo "calib write rc=$rc"; ok $rc cwrite
 fi
 echo "gpu_r5 $OUT done"

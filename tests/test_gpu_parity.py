@@ -121,7 +121,6 @@ def _edge_rays(sc, n_rand, n_edge, seed, tmax):
 
 TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
     "k_trace_lds": {},
-    "k_trace_lds_lanemask": {"PT_TRACE_VM": "0"},
     "k_trace_oct": {"PT_TRACE_OCT": "1"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
@@ -150,15 +149,17 @@ def test_frame_traversal_kernels_bit_exact(variant, monkeypatch, kernel, any_hit
     assert (nodes, prims) == (rnodes, rprims)
 
 
-@pytest.mark.parametrize("kernel", ["k_trace_lds", "k_trace_lds_lanemask"])
-@pytest.mark.parametrize("any_hit", [False, True])
-def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel, any_hit):
-    """k_trace_lds's one-comparison box test holds for tMax > the smallest
-    denormal; rays at or below it (0, +-denormals, the denormal range, NaN)
-    take the lane-mask steps.  Rays with such tMax values mixed into every
-    wave, and tMax values just around box distances: hits and node /
+@pytest.mark.parametrize("kernel", ["k_trace_lds", "k_trace_pt", "k_trace_nb_hbm"])
+def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel):
+    """The box test's tMax comparison (tMin < ray.tMax) at the edge values:
+    0, +-denormals, the denormal range, NaN, negative and random finite tMax
+    around box distances.  Shadow rays (the rays whose tMax the trace
+    kernels read from the record: closest-hit rays start at tMax = inf, as
+    SpawnRay's, interaction.h:66-69) with such tMax values mixed into every
+    wave, and tMax values around box distances: occlusion and node /
     primitive counters equal the oracle's (Bounds3::IntersectP,
     geometry.h:1584-1606, tMin < ray.tMax && tMax > 0)."""
+    any_hit = True
     for k, v in TRACE_KERNELS[kernel].items():
         monkeypatch.setenv(k, v)
     hs, sc = _scene(variant(**MINI))
@@ -169,11 +170,8 @@ def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel, any_hit):
     tm = np.where(pick < 0.15, tiny[rng.integers(len(tiny), size=len(rays))],
                   np.where(pick < 0.6, rng.uniform(0, 20, len(rays)).astype(np.float32), np.float32(np.inf)))
     rays[:, 6] = tm.astype(np.float32)
-    _, order = sc.bvh()
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
-    if not any_hit:
-        got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
     assert np.array_equal(got, ref)
     assert (nodes, prims) == (rnodes, rprims)
 
