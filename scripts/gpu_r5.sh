@@ -4,7 +4,8 @@
 #   STAGES (default "tests bench prof1 pmc sq"): any subset of tests bench ab prof prof1 pmc sq calib, run in that order
 #          prof1: kernel-trace --stats with PT_PIPES=1 (one pipeline: every launch runs alone, so the averages
 #          are kernel durations -- what the bench line's roofline uses); calib: tools/fetch_calib with
-#          FETCH_SIZE / WRITE_SIZE passes (scripts/fetch_calib_summary.py)
+#          FETCH_SIZE / WRITE_SIZE passes (scripts/fetch_calib_summary.py); icache: SQC instruction-cache
+#          hit / miss counters of the bench's kernels
 #   CFG    bench --config for bench/prof/pmc/sq (default c2); OUT tag (default $CFG)
 #   BARGS  extra bench args for prof/pmc (e.g. "--spp 64")
 # Outputs under gpurun_out/r5_$OUT/: source_hash.txt, pytest_gpu.log, smoke.log,
@@ -75,6 +76,13 @@ if has sq; then
     --output-format csv -- python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline $SQ \
     > "$o/sq2.log" 2>&1
   rc=$?; echo "pmc sq2 rc=$rc"; ok $rc sq2
+fi
+if has icache; then
+  # instruction-cache hits / misses of the bench's kernels (SQC block), beside the instruction counts
+  timeout -s KILL 150 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_INSTS_VALU \
+    SQ_INSTS_SALU SQ_WAVES -d "$o/pmc_ic" -o ic --output-format csv -- \
+    python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline ${SQARGS:---spp 16} > "$o/ic.log" 2>&1
+  rc=$?; echo "pmc icache rc=$rc"; ok $rc icache
 fi
 if has calib; then
   # FETCH_SIZE / WRITE_SIZE calibration: known bytes in the shading kernels' access shapes
