@@ -1245,6 +1245,165 @@ __global__ __launch_bounds__(1024) void k_film_s60_blk(DevHero h, DevPaths ps, F
 ;
 #endif
 
+// k_film_s60_sq<F>: the 60-bin film with one wave per F x F square of film
+// pixels, each source sample read once per square instead of once per film
+// pixel it reaches (k_film_s60: ~16 re-reads with the 2-pixel Gaussian, 36.5 GB
+// per C3h launch).  Lane = bin, as in k_film_s60; the square's K = F^2 FilmTile
+// contribSums are K registers per lane.  The wave walks the union of the K
+// filter windows FilmTile by FilmTile (tile row, tile column), source pixels in
+// scan order, samples in order -- every film pixel's own samples are a
+// subsequence of that walk, in its own order -- and at each FilmTile's end
+// converts each touched contribSum with ToXYZ and merges it (film.cpp:117-130),
+// as k_film_s60 does pixel by pixel.  No barrier: the wave loads each sample's
+// 240 B itself (four in flight).  A sample adds w = +0 to the film pixels it
+// does not reach (the weight is computed branch-free per film pixel): a sum that
+// starts at +0 and only ever adds finite values is never -0, so x + (+-0) == x
+// bit for bit (the sanitiser zeroes every sample with an infinite or NaN bin).
+template <int FX, int FY, int G>  // FX x FY film pixels per wave, G sample loads in flight
+__global__ __launch_bounds__(64) void k_film_s60_sq(DevHero h, DevPaths ps, FilmConsts fc,
+                                                    const int* __restrict__ pixslot, int p0, int np, int nsamp,
+                                                    int bx0, int by0, int bw, int bh, float4* accum)
+#ifdef PT_TU_HERO
+{
+    constexpr int K = FX * FY;
+    static_assert(K <= 32, "film pixels of a square fit the anyk bits and the wave");
+    __shared__ float s_tab[256];
+    const int lane = (int)lane_id();
+    for (int i = lane; i < 256; i += 64) s_tab[i] = fc.table[i];
+    __syncthreads();
+    const int nbx = (bw + FX - 1) / FX;
+    const int gx0 = bx0 + ((int)blockIdx.x % nbx) * FX, gy0 = by0 + ((int)blockIdx.x / nbx) * FY;
+    const int gx1 = min(gx0 + FX - 1, bx0 + bw - 1), gy1 = min(gy0 + FY - 1, by0 + bh - 1);
+    const int rx0 = max(gx0 - fc.win, fc.sb_x0), rx1 = min(gx1 + fc.win, fc.sb_x1 - 1);
+    const int ry0 = max(gy0 - fc.win, fc.sb_y0), ry1 = min(gy1 + fc.win, fc.sb_y1 - 1);
+    if (rx0 > rx1 || ry0 > ry1) return;
+    const int sbw = fc.sb_x1 - fc.sb_x0, cw = fc.crop_x1 - fc.crop_x0;
+    // film pixel k of the square is (gx0 + k % FX, gy0 + k / FX); lane k holds its accumulator
+    const int myx = gx0 + lane % FX, myy = gy0 + lane / FX;
+    const bool myon = lane < K && myx <= gx1 && myy <= gy1;
+    float4 acc = myon ? accum[(size_t)(myy - fc.crop_y0) * cw + (myx - fc.crop_x0)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool touched = false;
+    float binsum[K], wsum[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) binsum[k] = wsum[k] = 0.f;
+    uint32_t anyk = 0;  // film pixels the current FilmTile reached
+    for (int tr = (ry0 - fc.sb_y0) >> 4; tr <= (ry1 - fc.sb_y0) >> 4; ++tr) {
+        for (int tc = (rx0 - fc.sb_x0) >> 4; tc <= (rx1 - fc.sb_x0) >> 4; ++tc) {
+            const int qy0 = max(ry0, fc.sb_y0 + 16 * tr), qy1 = min(ry1, fc.sb_y0 + 16 * tr + 15);
+            const int qx0 = max(rx0, fc.sb_x0 + 16 * tc), qx1 = min(rx1, fc.sb_x0 + 16 * tc + 15);
+            for (int qy = qy0; qy <= qy1; ++qy) {
+                for (int qx = qx0; qx <= qx1; ++qx) {
+                    const int p = pixslot[(qy - fc.sb_y0) * sbw + (qx - fc.sb_x0)] - p0;
+                    if (p < 0 || p >= np) continue;
+                    // the square's film pixels whose window [t - win, t + win] holds q
+                    uint32_t wm = 0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int tx = gx0 + k % FX, ty = gy0 + k / FX;
+                        const bool in = tx <= gx1 && ty <= gy1 && qx >= tx - fc.win && qx <= tx + fc.win &&
+                                        qy >= ty - fc.win && qy <= ty + fc.win;
+                        wm |= in ? 1u << k : 0u;
+                    }
+                    if (!wm) continue;
+                    for (int c0 = 0; c0 < nsamp; c0 += 64) {
+                        const int sl = c0 + lane;
+                        uint32_t slot = 0;
+                        float ks = 1.f, dx = 0.f, dy = 0.f;
+                        int x0 = 1, x1 = 0, y0 = 1, y1 = 0;  // empty bounds: no film pixel
+                        if (sl < nsamp) {
+                            slot = (uint32_t)p * (uint32_t)nsamp + (uint32_t)sl;
+                            const float2 pf = ps.pfilm[slot];
+                            dx = pf.x - 0.5f;
+                            dy = pf.y - 0.5f;
+                            x0 = (int)ceilf(dx - fc.rx);
+                            x1 = (int)floorf(dx + fc.rx) + 1;
+                            y0 = (int)ceilf(dy - fc.ry);
+                            y1 = (int)floorf(dy + fc.ry) + 1;
+                            // radiance sanitiser (hero.cpp:118-140) and maxSampleLuminance
+                            const float yv = h.out_y[slot];  // -inf: a NaN bin
+                            if ((double)yv < -1e-5 || __builtin_isinf(yv)) ks = 0.f;
+                            else if (yv > fc.max_lum) ks = fc.max_lum / yv;
+                        }
+                        float wk[K];
+                        uint64_t mall = 0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int tx = gx0 + k % FX, ty = gy0 + k / FX;
+                            const bool touch = ((wm >> k) & 1u) && !(tx < x0 || tx >= x1 || ty < y0 || ty >= y1);
+                            float w = 0.f;
+                            if (touch) {
+                                const float fxv = fabsf((tx - dx) * fc.inv_rx * 16);
+                                const float fyv = fabsf((ty - dy) * fc.inv_ry * 16);
+                                int ix = (int)floorf(fxv); ix = ix < 15 ? ix : 15;
+                                int iy = (int)floorf(fyv); iy = iy < 15 ? iy : 15;
+                                w = s_tab[iy * 16 + ix];
+                            }
+                            wk[k] = w;
+                            const uint64_t mk = __ballot(touch);
+                            anyk |= mk ? 1u << k : 0u;
+                            mall |= mk;
+                        }
+                        // the samples that reach any film pixel of the square, in order, G per round
+                        while (mall) {
+                            int js[G];
+                            float vs[G];
+#pragma unroll
+                            for (int u = 0; u < G; ++u) {
+                                js[u] = mall ? __ffsll((unsigned long long)mall) - 1 : -1;
+                                mall &= mall - 1;
+                                const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)slot, js[u] < 0 ? 0 : js[u]);
+                                vs[u] = (js[u] >= 0 && lane < kNS) ? h.out60[(size_t)sj * kNS + lane] : 0.f;
+                            }
+#pragma unroll
+                            for (int u = 0; u < G; ++u) {
+                                if (js[u] < 0) break;
+                                const float kj = lane_val(ks, js[u]);
+                                float v = vs[u];
+                                if (kj == 0.f) v = 0.f;        // L = Spectrum(0.f)
+                                else if (kj != 1.f) v = v * kj;  // L *= maxSampleLuminance / L.y()
+#pragma unroll
+                                for (int k = 0; k < K; ++k) {
+                                    const float wj = lane_val(wk[k], js[u]);  // +0 where the sample misses k
+                                    binsum[k] += (v * 1.f) * wj;
+                                    wsum[k] += wj;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            // the FilmTile's end: ToXYZ of each reached film pixel's contribSum, merged in tile order
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if ((anyk >> k) & 1u) {
+                    float x = 0.f, y = 0.f, z = 0.f;
+                    for (int i = 0; i < kNS; ++i) {
+                        const float c = lane_val(binsum[k], i);
+                        x += h.XYZ[i] * c;
+                        y += h.XYZ[kNS + i] * c;
+                        z += h.XYZ[2 * kNS + i] * c;
+                    }
+                    const float scale = (float)(700 - 400) / (float)(106.856895f * kNS);
+                    if (lane == k) {
+                        acc.x += x * scale;
+                        acc.y += y * scale;
+                        acc.z += z * scale;
+                        acc.w += wsum[k];
+                        touched = true;
+                    }
+                }
+                binsum[k] = 0.f;
+                wsum[k] = 0.f;
+            }
+            anyk = 0;
+        }
+    }
+    if (touched && myon) accum[(size_t)(myy - fc.crop_y0) * cw + (myx - fc.crop_x0)] = acc;
+}
+#else
+;
+#endif
+
 // SpatialLightDistribution::ComputeDistribution (lightdistrib.cpp:175-236)
 // for every voxel: 128 radical-inverse points, each light's Li.y() / pdf,
 // floored at 0.001 x the average, as a Distribution1D (sampling.h:65-88).

@@ -291,6 +291,7 @@ struct pt_scene {
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
     int film_blk = 0;            // hero film: PT_FILM_BLK=1 takes the LDS-staged k_film_s60_blk (slower: DESIGN §10)
+    int film_sq = 1;             // hero film: k_film_s60_sq over 2 x 2 film-pixel squares (PT_FILM_SQ=0: k_film_s60 per pixel)
     int film_sk = -1;            // RGB film: k_film_sk (skewed lane-per-pixel walks) for win 2 (-1, default: C3's 2-pixel
                                  // Gaussian 20.5 -> 5.1 ms per launch), PT_FILM_SK=1 also for win 1 (box: equal), 0 never
     int film_skew = 1;           // k_film_sk: PT_FILM_SKEW=0/1/2 -- the lanes' walks unskewed / skewed by column / by column and row
@@ -1404,7 +1405,12 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
             const int bw = g.bx1 - g.bx0, bh = g.by1 - g.by0;
             if (bw > 0 && bh > 0) {
                 const dim3 fg(std::max(1, std::min(ceil_div(bw * bh, 4), s->num_cus * 32)));
-                if (s->hero && s->film_blk && s->film.win <= kF60MaxWin)
+                if (s->hero && s->film_sq && !s->film_blk) {
+                    // k_film_s60_sq: one wave per 2 x 2 film pixels, 16 sample loads in flight (C3h: 2 x 2 beat
+                    // 3 x 2, 4 x 2 and 3 x 3 squares, and 16 loads beat 4 and 8)
+                    hipLaunchKernelGGL((k_film_s60_sq<2, 2, 16>), dim3(ceil_div(bw, 2) * ceil_div(bh, 2)), dim3(64), 0, st,
+                                       hh, ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);
+                } else if (s->hero && s->film_blk && s->film.win <= kF60MaxWin)
                     hipLaunchKernelGGL(k_film_s60_blk, dim3(ceil_div(bw, 8) * ceil_div(bh, 8)), dim3(1024), 0, st, hh,
                                        ps, s->film, dslot.p, g.p0, g.np, ns, g.bx0, g.by0, bw, bh, d_accum);
                 else if (s->hero)
@@ -1676,6 +1682,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                      : s->trace_persist                                                            ? "k_trace_pt"
                                                                                                    : "k_trace");
     if (const char* t = std::getenv("PT_FILM_BLK")) s->film_blk = std::atoi(t);
+    if (const char* t = std::getenv("PT_FILM_SQ")) s->film_sq = std::atoi(t);
     if (const char* t = std::getenv("PT_FILM_T")) s->film_t = std::atoi(t);
     if (const char* t = std::getenv("PT_FILM_SK")) s->film_sk = std::atoi(t);
     if (const char* t = std::getenv("PT_FILM_SKEW")) s->film_skew = std::min(2, std::max(0, std::atoi(t)));

@@ -19,4 +19,7 @@ PT_HERO_FT(kFtMicro | kFtSpecular | kFtInfinite)
 PT_HERO_FT(kFtAll)
 #undef PT_HERO_FT
 #undef PT_ARGS
+#define PT_FILM_ARGS DevHero, DevPaths, FilmConsts, const int*, int, int, int, int, int, int, int, float4*
+template __global__ void k_film_s60_sq<2, 2, 16>(PT_FILM_ARGS);
+#undef PT_FILM_ARGS
 }  // namespace pt

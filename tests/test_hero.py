@@ -276,7 +276,10 @@ def test_hero_film_staged_matches_oracle(tmp_path, filt, spp):
     == the oracle, bit for bit; and the opt-in LDS-staged k_film_s60_blk
     (PT_FILM_BLK=1: several 128-sample chunks per source pixel at 136 spp, a
     partial chunk at 70 spp; a window above kF60MaxWin, gaussian radius 6,
-    falls back to k_film_s60) gives the identical film."""
+    falls back to k_film_s60) give the identical film; the default film is
+    k_film_s60_sq (2 x 2 squares, cut by the batch box and the crop window,
+    windows reaching two or four FilmTiles) and PT_FILM_SQ=0 the per-pixel
+    k_film_s60, bit-identical."""
     txt = open(_c3_variant(tmp_path, "hero_path_mis", res=24, spp=spp)).read()
     txt = re.sub(r'"integer xresolution" \[\d+\]', '"integer xresolution" [37]', txt)
     txt = txt.replace('Film "image"', 'Film "image" "float cropwindow" [0.05 0.93 0.1 0.85]')
@@ -299,3 +302,11 @@ def test_hero_film_staged_matches_oracle(tmp_path, filt, spp):
     finally:
         del os.environ["PT_FILM_BLK"]
     assert np.array_equal(staged.view(np.uint32), got.view(np.uint32))
+    # the default k_film_s60_sq (one wave per 2 x 2 film pixels walking the union of their windows) against the
+    # per-pixel k_film_s60 (PT_FILM_SQ=0)
+    os.environ["PT_FILM_SQ"] = "0"
+    try:
+        per_pixel, _ = ptgpu.Scene(hs, batch_slots=slots).render()
+    finally:
+        del os.environ["PT_FILM_SQ"]
+    assert np.array_equal(per_pixel.view(np.uint32), got.view(np.uint32))
