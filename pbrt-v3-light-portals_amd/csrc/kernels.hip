@@ -334,11 +334,13 @@ __device__ __forceinline__ bool node_box_hit(float4 a, float4 b, const Ray& ray,
     return ok1 & ok2 & (tMin < ray.tmax) & (tMax > 0);
 }
 
-// PT_TRACE_PT_WAVES (experiment builds): force the waves-per-SIMD register budget
+// 7 waves per SIMD without spheres (72 VGPRs: the one-register stack position below brought the
+// kernel from 78 to 74, and the remaining 12 B of spills are reloaded once per primitive test; C5
+// isolated 52.7 -> 49.4 ms per launch); PT_TRACE_PT_WAVES (experiment builds) overrides
 #ifdef PT_TRACE_PT_WAVES
 #define PT_TRACE_PT_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_PT_WAVES)))
 #else
-#define PT_TRACE_PT_ATTR
+#define PT_TRACE_PT_ATTR __attribute__((amdgpu_waves_per_eu(kSph ? 1 : 7)))
 #endif
 template <bool kLdsScene, bool kSpill, bool kSph>
 __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevScene sc, DevPaths ps, const uint32_t* __restrict__ rq,
@@ -367,16 +369,28 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
     const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
     const int tid = threadIdx.x;
     const uint32_t lane = lane_id();
-    int* myspill = spill + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * 64;
-    uint32_t nodes = 0, prims = 0, ncl = 0, nsh = 0, iters = 0;  // per lane per launch: fit 32 bits
+    // The stack position as ONE register: so = toVisit * 512 + 4 * tid, the byte offset of the lane's next
+    // free LDS stack entry ([row][kTraceBlock] ints, rows 512 bytes apart) -- its depth is so >> 9, its
+    // column so & 511 -- instead of the depth plus the thread index (which the 7-wave budget, 72 VGPRs,
+    // otherwise spilled).  Entries past the LDS rows go to the lane's spill column, entry v at spill[SPILL(v)].
+    static_assert(kTraceBlock * 4 == 512, "k_trace_pt stack rows are 512 bytes apart");
+#define SPILL(v) ((blockIdx.x * (uint32_t)kTraceBlock + ((so & 511u) >> 2)) * 64u + (uint32_t)(v))
+#define STK(o) (*reinterpret_cast<int*>(reinterpret_cast<char*>(stk) + (o)))
+    // per lane per launch: nodes / prims fit 32 bits, rays 16 bits each (closest | shadow << 16); the loop
+    // count is the wave's (uniform, a scalar register)
+    uint32_t nodes = 0, prims = 0, nrays = 0;
+    uint32_t iters_w = 0;
     bool active = false, exhausted = false, drained = false;
     uint32_t qn = 0, qe = 0;  // the wave's private chunk of the ray queue (as k_trace_nb)
-    uint32_t slot = 0, kind = 0;
+    uint32_t ent = 0;  // the ray-queue entry: slot << 2 | kind (one register for both)
     Ray ray{v3(0, 0, 0), v3(0, 0, 1), 0};
     V3 inv = v3(0, 0, 0);
     TriShear sh{0, 0, 0, 0};
     bool n0 = false, n1 = false, n2 = false;
-    int cur = 0, toVisit = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
+    const uint32_t so0 = 4u * (uint32_t)tid;  // an empty stack
+    uint32_t so = so0;
+    const uint32_t soRows = (uint32_t)stack_rows * 512u;
+    int cur = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
     for (;;) {
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
@@ -398,13 +412,13 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 if (!active) {
                     if (k < take) {
                         const uint32_t e = rq[i];
-                        slot = e >> 2;
-                        kind = e & 3u;
+                        ent = e;
+                        const uint32_t slot = e >> 2, kind = e & 3u;
                         ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA), slot, kind == kRayShadow);
                         inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
                         sh = tri_shear(ray.d);
                         n0 = inv.x < 0; n1 = inv.y < 0; n2 = inv.z < 0;
-                        cur = 0; toVisit = 0; hitPrim = -1; leafPos = 0; leafEnd = 0;
+                        cur = 0; so = so & 511u; hitPrim = -1; leafPos = 0; leafEnd = 0;
                         active = sc.n_nodes > 0;  // empty scene: every ray misses
                         if (!active) {
                             if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
@@ -412,7 +426,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                             else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
                             else *hit_word(ps, slot, kHdHitB) = -1;
                         }
-                        if (kind == kRayShadow) ++nsh; else ++ncl;
+                        nrays += kind == kRayShadow ? 0x10000u : 1u;
                     }
                 }
             }
@@ -429,7 +443,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
         const uint32_t nLeaf = (uint32_t)__popcll(__ballot(wantLeaf));
         const uint32_t nNode = (uint32_t)__popcll(__ballot(active && !wantLeaf));
         const bool leafStep = nLeaf >= (nNode == 0 ? 1u : lmin);  // lmin >= 1
-        ++iters;
+        ++iters_w;
         if (!active || wantLeaf != leafStep) continue;
         bool done = false;
         if (leafStep) {
@@ -448,18 +462,18 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 } else {
                     const float4 r2 = bprims[3 * pi + 2];
                     ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
-                    if (kind != kRayShadow && (fl & kPrimDegenerate)) ok = false;
+                    if ((ent & 3u) != kRayShadow && (fl & kPrimDegenerate)) ok = false;
                 }
                 if (ok) {
                     hitPrim = pi;
-                    if (kind == kRayShadow) done = true;
+                    if ((ent & 3u) == kRayShadow) done = true;
                     else ray.tmax = t;
                 }
                 if (!done && leafPos == leafEnd) {
-                    if (toVisit == 0) done = true;
+                    if (so < 512u) done = true;
                     else {
-                        --toVisit;
-                        cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
+                        so -= 512u;
+                        cur = (!kSpill || so < soRows) ? STK(so) : spill[SPILL((so >> 9) - (uint32_t)stack_rows)];
                     }
                 }
             }
@@ -482,19 +496,20 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                         const bool neg = axis == 0 ? n0 : (axis == 1 ? n1 : n2);
                         const int far = neg ? cur + 1 : off;
                         cur = neg ? off : cur + 1;
-                        if (!kSpill || toVisit < stack_rows) stk[toVisit * kTraceBlock + tid] = far;
-                        else myspill[toVisit - stack_rows] = far;
-                        ++toVisit;
+                        if (!kSpill || so < soRows) STK(so) = far;
+                        else spill[SPILL((so >> 9) - (uint32_t)stack_rows)] = far;
+                        so += 512u;
                     }
-                } else if (toVisit == 0) {
+                } else if (so < 512u) {
                     done = true;
                 } else {
-                    --toVisit;
-                    cur = (!kSpill || toVisit < stack_rows) ? stk[toVisit * kTraceBlock + tid] : myspill[toVisit - stack_rows];
+                    so -= 512u;
+                    cur = (!kSpill || so < soRows) ? STK(so) : spill[SPILL((so >> 9) - (uint32_t)stack_rows)];
                 }
             }
         }
         if (done) {
+            const uint32_t slot = ent >> 2, kind = ent & 3u;
             if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
             else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
             else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
@@ -502,9 +517,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
             active = false;
         }
     }
-    flush_stats(stats, ncl, nsh, nodes, prims);
-    const unsigned long long itw = wave_sum_u64(iters);
-    if (lane == 0 && itw) atomicAdd(&stats->lane_iters, itw);
+    flush_stats(stats, nrays & 0xffffu, nrays >> 16, nodes, prims);
+    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
+#undef SPILL
+#undef STK
 }
 #else
 ;
