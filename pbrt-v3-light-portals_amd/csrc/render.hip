@@ -273,7 +273,7 @@ struct pt_scene {
     int pipes = 2;                 // pipelines render_tiles runs batches on (PT_PIPES)
     int device = 0;
     int num_cus = 256;
-    size_t target_slots = 0;  // batch size in camera samples; 0: 64 M (8 M for the 60-bin hero state)
+    size_t target_slots = 0;  // batch size in camera samples; 0: 96 M (8 M for the 60-bin hero state)
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
@@ -1223,7 +1223,8 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         int bx0, by0, bx1, by1;
     };
     std::vector<Group> groups;
-    size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)64 << 20);
+    // 96 M camera samples (C2: 64 M 877, 96 M 897, 128 M 896, 160 M 896 Msamples/s, same box)
+    size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)96 << 20);
     {   // a render of only a few batches (one rank's shard of a multi-GPU frame) is split into equal batches, a
         // multiple of the pipelines, so the pipelines finish together instead of one running a short remainder
         // batch alone (PT_BATCH_EQUAL=<max batches>, 0 = off)

@@ -787,7 +787,7 @@ def test_film_max_sample_luminance_matches_oracle(tmp_path, monkeypatch, film_sk
 
 def test_full_config_sparse_tiles_bit_exact():
     """Parity at the benchmarked configuration: the C2 scene as benchmarked
-    (1920x1080 @256 spp, path maxdepth 5, the default 64 M-slot batches and
+    (1920x1080 @256 spp, path maxdepth 5, the default 96 M-slot batches and
     two pipelines) on the tiles t % 400 == 0 spread over the whole frame,
     against the oracle's film of the same tiles (SamplerIntegrator::Render,
     integrator.cpp:526-637) -- bit-identical film and identical counters."""
