@@ -246,7 +246,7 @@ constexpr uint32_t kStCont = 1u << 21;       // continuation ray pending
 constexpr uint32_t kStNee = 1u << 22;        // NEE payload pending
 constexpr uint32_t kStDimOverflow = 1u << 23;
 constexpr uint32_t kStNfShift = 24;          // kNf* << 24
-constexpr uint32_t kStNfMask = 0x3fu << kStNfShift;
+constexpr uint32_t kStNfMask = 0x7fu << kStNfShift;
 
 // NEE payload: kNee floats per slot (ps.nee[kNee * slot + k]), four 16-B
 // quarters read as the resolve needs them
@@ -267,6 +267,7 @@ constexpr uint32_t kNfA = 4u;          // ray A traced
 constexpr uint32_t kNfB = 8u;          // ray B traced
 constexpr uint32_t kNfDivPortal = 16u; // divide by portal pdf (projection strategy)
 constexpr uint32_t kNfC1 = 32u;        // MIS light contribution present (needs unoccluded A)
+constexpr uint32_t kNfLi0 = 64u;       // portal kinds: the Li fallback on a miss is zero (quarter 2 not written)
 
 // Ray queue entry kinds (low 2 bits)
 constexpr uint32_t kRayCont = 0, kRayA = 1, kRayShadow = 2, kRayB = 3;

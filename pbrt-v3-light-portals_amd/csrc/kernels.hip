@@ -1327,7 +1327,7 @@ __device__ __forceinline__ NeeIn nee_load(const DevPaths& ps, uint32_t slot, uin
         in.F = s3(q1.x, q1.y, q1.z);
         if (portalA) in.pdf = q1.w;
     }
-    if ((portalA && hA < 0) || misB) {  // Li / f2, the MIS scattering weight
+    if ((portalA && hA < 0 && !(fl & kNfLi0)) || misB) {  // Li / f2, the MIS scattering weight
         const float4 q2 = q[2];
         in.Li = s3(q2.x, q2.y, q2.z);
         if (misB) in.w = q2.w;
@@ -1486,9 +1486,10 @@ __device__ __forceinline__ uint32_t portal_nee(const DevScene& sc, const DevPath
                     store_ray(ps.rayA, slot, r);
                     put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
                     put_nee(ps, slot, kNeePdf, pdf);
-                    put_nee3(ps, slot, kNeeLi, s3(0.f));
-                    flags |= kNfA;
-                    if (ab) *ab += 24 + 12 + 4 + 12;
+                    // Li = 0 before the portal ray is traced (portal_arealight.cpp:181), kept on a miss: a flag
+                    // instead of a 12-B store and load
+                    flags |= kNfA | kNfLi0;
+                    if (ab) *ab += 24 + 12 + 4 + 12;  // the algorithmic count keeps Li's 12 B
                 }
                 return flags;
             }
