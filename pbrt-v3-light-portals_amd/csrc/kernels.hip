@@ -1817,8 +1817,19 @@ __device__ __forceinline__ DevScene stage_tables(const DevScene& sc, uint4* lds)
 // register, which the 3-wave build cannot spare, so the counting build is a
 // separate instantiation that the renderer runs only on request
 // (pt_set_count_bytes; the bench's one extra frame).
+// kAhead: the NEE payload and the hit primitive's record (path_load_now) are
+// loaded one path ahead as well, with the next path's body, instead of at the
+// start of the path's own step -- ≈30 more VGPRs, for the 2-wave MIS kernels
+// whose feature set leaves them (ShadeAhead)
 #define PT_ABP (kAb ? &ab : nullptr)
-template <int kFt, bool kTab, bool kLean = false, bool kAb = false>
+#ifdef PT_NO_AHEAD  // experiment build: the round-4 order
+template <int kFt>
+constexpr bool kShadeAhead = false;
+#else
+template <int kFt>
+constexpr bool kShadeAhead = Ft<kFt>::mis && kFt != kFtAll;  // kFtAll: 228 -> 256 VGPRs, one wave
+#endif
+template <int kFt, bool kTab, bool kLean = false, bool kAb = false, bool kAhead = false>
 __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
@@ -1897,13 +1908,25 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         path_prefetch_head<Ft<kFt>::mis>(ps, slot1, &nxt);
     }
     if (i0 + 2 * stride < n) slot2 = pq[i0 + 2 * stride];
+    PathNow now{};  // kAhead: this path's NEE payload and hit record, loaded one path ahead
+    if constexpr (kAhead) {
+        if (i0 < n) path_load_now<kFt>(sc, ps, slot, pre, &now);
+    }
     for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
         PathPre nn{};
-        PathNow now{};
         uint32_t slot3 = 0;
-        if (i < n) path_load_now<kFt>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
-        if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
+        PathNow nowN{};
+        if constexpr (kAhead) {
+            if (i + stride < n) {
+                path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
+                path_load_now<kFt>(sc, ps, slot1, nxt, &nowN);
+            }
+        } else {
+            now = PathNow{};
+            if (i < n) path_load_now<kFt>(sc, ps, slot, pre, &now);  // issued ahead of the prefetches below
+            if (i + stride < n) path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
+        }
         if (i + 2 * stride < n) path_prefetch_head<Ft<kFt>::mis>(ps, slot2, &nn);
         if (i + 3 * stride < n) slot3 = pq[i + 3 * stride];
         RayList rays;
@@ -1915,6 +1938,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         slot2 = slot3;
         pre = nxt;
         nxt = nn;
+        if constexpr (kAhead) now = nowN;
     }
     }
 #endif
@@ -2220,7 +2244,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene sc, DevPaths ps,
                                                        uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, false, false, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, false, false, kAb, kShadeAhead<kFt>>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;
@@ -2233,7 +2257,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_tab(DevScene sc, DevPaths
                                                            uint32_t* pq_out_count, DevStats* stats)
 #ifdef PT_TU_SHADE
 {
-    shade_batch<kFt, true, false, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+    shade_batch<kFt, true, false, kAb, kShadeAhead<kFt>>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
 }
 #else
 ;
