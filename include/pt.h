@@ -403,9 +403,10 @@ pt_status pt_render_range_accum(pt_scene* scene, int tile_offset, int tile_strid
  * limit (~252M slots; ~70M for hero scenes) are PT_ERR_INVALID_ARG. */
 pt_status pt_set_batch_slots(pt_scene* scene, int64_t slots);
 
-/* Batches in flight (default 2): each pipeline is a host thread, a stream
- * and its own path-state buffers; one batch's trace kernel overlaps another's
- * shading.  1 runs the batches one after the other (isolated kernel timings). */
+/* Batches in flight (default 2 for scenes whose BVH fits LDS, 1 for BVHs
+ * traversed from HBM): each pipeline is a host thread, a stream and its own
+ * path-state buffers; one batch's trace kernel overlaps another's shading.
+ * 1 runs the batches one after the other (isolated kernel timings). */
 pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
 /* Count the shading kernel's algorithmic path-state bytes (pt_stats.shade_bytes)
  * in the renders that follow (default off: the count costs the 3-waves-per-SIMD

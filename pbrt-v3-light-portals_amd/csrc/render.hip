@@ -1640,6 +1640,11 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     const char* e = std::getenv("PT_TRACE_LDS");
     s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                              ? scene_bytes : 0;
+    // A BVH traversed from HBM (k_trace_pt) renders its batches on one pipeline: that traversal is bound
+    // by the latency of its node fetches at 7 waves per SIMD, and a shading launch beside it takes waves
+    // and memory bandwidth from it (C5: 168.4 / 167.9 vs 163.4 / 163.7 Msamples/s); the
+    // LDS-resident scenes keep two (C2 / C3 / C4 gain 2-12 %)
+    if (!s->lds_scene_bytes) s->pipes = 1;
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) {

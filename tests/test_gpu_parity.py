@@ -827,6 +827,25 @@ def test_batch_equal_two_pipelines_bit_exact(tmp_path, monkeypatch, equal):
             assert gst[k] == rst[k], k
 
 
+def test_default_pipelines_follow_bvh_residency(tmp_path, monkeypatch):
+    """Two pipelines by default for a BVH in LDS, one for a BVH traversed from
+    HBM (PT_TRACE_LDS=0 forces it; C5's case), and both render the oracle's
+    film bit for bit."""
+    from conftest import scene_variant
+    monkeypatch.delenv("PT_PIPES", raising=False)
+    path = scene_variant(tmp_path, name="portal_cornell.pbrt", res=(64, 48), spp=4)
+    hs = ptgpu.HostScene(path)
+    ref, rst = pyoracle.render_accum(hs.desc, nthreads=8)
+    for lds, pipes in (("1", 2), ("0", 1)):
+        monkeypatch.setenv("PT_TRACE_LDS", lds)
+        sc = ptgpu.Scene(hs, batch_slots=16 * 16 * 4 * 3)
+        assert sc.query("pipelines") == pipes
+        got, gst = sc.render_accum(0, 1)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        for k in ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
+            assert gst[k] == rst[k], k
+
+
 def test_count_bytes_build_renders_the_same(variant):
     """pt_set_count_bytes switches to the shading build that counts the
     algorithmic path-state bytes: the same image and counters, shade_bytes > 0
