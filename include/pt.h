@@ -426,7 +426,7 @@ enum pt_scene_key {
     PT_Q_FEATURES = 4,         /* scene-feature set the shading kernel is instantiated for */
     PT_Q_TRACE_KERNEL = 5,     /* traversal kernel of a render: 0 k_trace, 1 k_trace_pt, 2 k_trace_nb, 3 k_trace_lds,
                                   5 k_trace_oct */
-    PT_Q_SHADE_KERNEL = 6      /* shading kernel: 0 k_shade, 3 k_shade_w3, 5 k_shade_tab, 6 k_shade_dl,
+    PT_Q_SHADE_KERNEL = 6      /* shading kernel: 0 k_shade, 3 k_shade_w3, 4 k_shade_w3h, 5 k_shade_tab, 6 k_shade_dl,
                                   7 / 8 / 9 k_shade_hero / _w2 / _w4 */
 };
 pt_status pt_scene_query(const pt_scene* scene, int32_t key, int64_t* value);

@@ -2262,6 +2262,18 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade_tab(DevScene sc, DevPaths
 #else
 ;
 #endif
+// k_shade with a 3-waves-per-SIMD register budget (scene tables too large for LDS)
+template <int kFt, bool kAb>
+__global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3h(
+    DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq, const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
+    uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count, DevStats* stats)
+#ifdef PT_TU_SHADE
+{
+    shade_batch<kFt, false, Ft<kFt>::mis, kAb>(sc, ps, pq, pq_count, rq_out, rq_out_count, pq_out, pq_out_count, stats);
+}
+#else
+;
+#endif
 // k_shade_tab with a 3-waves-per-SIMD register budget (PT_SHADE_VARIANT=3)
 template <int kFt, bool kAb>
 __global__ __launch_bounds__(kShadeBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_shade_w3(

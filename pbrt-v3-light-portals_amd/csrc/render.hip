@@ -281,7 +281,8 @@ struct pt_scene {
     int hero_waves = 2;          // k_shade_hero register budget (PT_HERO_WAVES=1|2|4); C3h: 2 > 4 > 1
     bool count_bytes = false;    // pt_set_count_bytes: the shading build that counts algorithmic path-state bytes
     int shade_variant = 0;       // 0: compiler register budget, 3: k_shade_tab at 3 waves per SIMD (default when
-                                 // that build has no scratch), 5: k_shade_tab
+                                 // that build has no scratch), 4: k_shade at 3 waves per SIMD (the same, tables
+                                 // too large for LDS), 5: k_shade_tab
     int features = pt::kFtAll;   // scene features the shading kernel is compiled for (kFt*)
     bool has_spheres = true;     // trace kernels with the sphere test
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
@@ -358,6 +359,7 @@ template <int kFt>
 static ShadeKernel shade_kernel_ft(int variant, bool ab) {
     switch (variant) {
         case 3: return ab ? k_shade_w3<kFt, true> : k_shade_w3<kFt, false>;
+        case 4: return ab ? k_shade_w3h<kFt, true> : k_shade_w3h<kFt, false>;
         case 5: return ab ? k_shade_tab<kFt, true> : k_shade_tab<kFt, false>;
         default: return ab ? k_shade<kFt, true> : k_shade<kFt, false>;
     }
@@ -1649,13 +1651,13 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) {
         s->shade_variant = std::atoi(v);
-        if (s->shade_variant != 0 && s->shade_variant != 3 && s->shade_variant != 5)
-            throw PtError(PT_ERR_INVALID_ARG, "PT_SHADE_VARIANT must be 0, 3 or 5");
+        if (s->shade_variant != 0 && s->shade_variant != 3 && s->shade_variant != 4 && s->shade_variant != 5)
+            throw PtError(PT_ERR_INVALID_ARG, "PT_SHADE_VARIANT must be 0, 3, 4 or 5");
         // k_shade_w3 and k_shade_tab stage the scene tables in LDS: without room for them (tables larger
         // than kTabLdsMax, or PT_SHADE_TAB=0) the launch's dynamic LDS holds only the Halton tables, so
         // those builds would copy past their allocation -- take k_shade instead
-        if (!s->shade_tab) s->shade_variant = 0;
-        if (s->shade_variant == 3) s->shade_bpc = kShadeBpcW3;
+        if (!s->shade_tab && s->shade_variant != 4) s->shade_variant = 0;
+        if (s->shade_variant == 3 || s->shade_variant == 4) s->shade_bpc = kShadeBpcW3;
     } else if (s->shade_tab && !s->hero && s->features == kFtPortalOnly) {
         // the 3-waves-per-SIMD build of k_shade_tab when it needs no scratch (spills cost more than the
         // third wave gains), with the grid-stride loop sized for it (PT_SHADE_BPC overrides).  Only for
@@ -1665,6 +1667,13 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, (const void*)shade_kernel(3, s->features)) == hipSuccess && fa.localSizeBytes == 0) {
             s->shade_variant = 3;
+            s->shade_bpc = kShadeBpcW3;
+        }
+    } else if (!s->shade_tab && !s->hero && s->features == kFtPortalOnly) {
+        // the same 3-wave build with the scene tables read from HBM (C5's ten million primitive records)
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, (const void*)shade_kernel(4, s->features)) == hipSuccess && fa.localSizeBytes == 0) {
+            s->shade_variant = 4;
             s->shade_bpc = kShadeBpcW3;
         }
     }

@@ -12,6 +12,8 @@ namespace pt {
     template __global__ void k_shade<F, false>(PT_ARGS);     \
     template __global__ void k_shade_tab<F, false>(PT_ARGS); \
     template __global__ void k_shade_w3<F, false>(PT_ARGS);  \
+    template __global__ void k_shade_w3h<F, false>(PT_ARGS); \
+    template __global__ void k_shade_w3h<F, true>(PT_ARGS);  \
     template __global__ void k_shade<F, true>(PT_ARGS);      \
     template __global__ void k_shade_tab<F, true>(PT_ARGS);  \
     template __global__ void k_shade_w3<F, true>(PT_ARGS);

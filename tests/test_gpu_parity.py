@@ -288,6 +288,8 @@ SHADE_VARIANTS = [
     {"PT_SHADE_VARIANT": "3"},                          # k_shade_w3 (MIS scenes: the kLean 3-wave build)
     {"PT_SHADE_VARIANT": "3", "PT_SHADE_TAB": "0"},     # no table room: falls back to k_shade
     {"PT_SHADE_VARIANT": "5", "PT_SHADE_TAB": "0"},
+    {"PT_SHADE_VARIANT": "4"},                          # k_shade_w3h: 3 waves, scene tables from HBM
+    {"PT_SHADE_TAB": "0"},                              # default without table room (C5: k_shade_w3h if portal-only)
 ]
 
 
@@ -305,6 +307,9 @@ def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
         monkeypatch.setenv(k, v)
     path = scene_variant(tmp_path, name=scene, res=(48, 32), spp=8)
     hs, sc = _scene(path)
+    if env == {"PT_SHADE_TAB": "0"}:
+        assert sc.kernel_names()[1] == {"portal_cornell.pbrt": "k_shade_w3h", "portal_room.pbrt": "k_shade",
+                                        "lamp/lamp.pbrt": "k_shade_dl"}[scene]
     got, gst = sc.render()
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
@@ -313,7 +318,7 @@ def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
 
 
 def test_shade_variant_rejects_unknown(variant, monkeypatch):
-    monkeypatch.setenv("PT_SHADE_VARIANT", "4")
+    monkeypatch.setenv("PT_SHADE_VARIANT", "7")
     hs = ptgpu.HostScene(variant(**MINI))
     with pytest.raises(ptgpu.PtError, match="PT_SHADE_VARIANT"):
         ptgpu.Scene(hs)
