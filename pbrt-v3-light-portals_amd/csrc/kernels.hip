@@ -378,7 +378,12 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
 #define STK(o) (*reinterpret_cast<int*>(reinterpret_cast<char*>(stk) + (o)))
     // per lane per launch: nodes / prims fit 32 bits, rays 16 bits each (closest | shadow << 16); the loop
     // count is the wave's (uniform, a scalar register)
-    uint32_t nodes = 0, prims = 0, nrays = 0;
+    // The counters as wave totals (uniform: scalar registers).  A lane's node visits and primitive tests of
+    // one loop iteration (cst: visits in bits 0-3, tests in bits 8-11) are added at the top of the next,
+    // where the wave's lanes are converged, one ballot per bit; rays where the refill takes them.
+    static_assert(kNodeSteps < 16 && kLeafSteps < 16, "k_trace_pt step counts are 4-bit fields");
+    uint32_t ncl_w = 0, nsh_w = 0, nodes_w = 0, prims_w = 0;
+    uint32_t cst = 0;
     uint32_t iters_w = 0;
     bool active = false, exhausted = false, drained = false;
     uint32_t qn = 0, qe = 0;  // the wave's private chunk of the ray queue (as k_trace_nb)
@@ -392,6 +397,12 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
     const uint32_t soRows = (uint32_t)stack_rows * 512u;
     int cur = 0, hitPrim = -1, leafPos = 0, leafEnd = 0;
     for (;;) {
+#pragma unroll
+        for (int bit = 0; bit < 4; ++bit) {
+            if ((1 << bit) <= kNodeSteps) nodes_w += (uint32_t)__popcll(__ballot((cst >> bit) & 1u)) << bit;
+            if ((1 << bit) <= kLeafSteps) prims_w += (uint32_t)__popcll(__ballot((cst >> (8 + bit)) & 1u)) << bit;
+        }
+        cst = 0;
         if (!exhausted) {
             const uint64_t idle = __ballot(!active);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -409,6 +420,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 const uint32_t i = qn + k;
                 qn += take;
                 if (drained && qn >= qe) exhausted = true;
+                const bool takes = !active && k < take;  // exactly `take` idle lanes
                 if (!active) {
                     if (k < take) {
                         const uint32_t e = rq[i];
@@ -426,9 +438,11 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                             else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
                             else *hit_word(ps, slot, kHdHitB) = -1;
                         }
-                        nrays += kind == kRayShadow ? 0x10000u : 1u;
                     }
                 }
+                const uint32_t nsh = (uint32_t)__popcll(__ballot(takes && (ent & 3u) == kRayShadow));
+                nsh_w += nsh;
+                ncl_w += take - nsh;
             }
         }
         if (__ballot(active) == 0) {
@@ -451,7 +465,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
             for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
                 if (u > 0 && (done || leafPos >= leafEnd)) continue;
                 const int pi = leafPos++;
-                ++prims;
+                cst += 0x100u;
                 const float4 r0 = bprims[3 * pi];
                 const float4 r1 = bprims[3 * pi + 1];
                 const uint32_t fl = __float_as_uint(r0.w);
@@ -483,7 +497,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
                 if (u > 0 && (done || leafPos < leafEnd)) continue;
                 const float4 a = bnodes[2 * cur];
                 const float4 b = bnodes[2 * cur + 1];
-                ++nodes;
+                ++cst;
                 if (node_box_hit(a, b, ray, inv, n0, n1, n2)) {
                     const int off = __float_as_int(b.z);
                     const uint32_t npax = __float_as_uint(b.w);
@@ -517,8 +531,13 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
             active = false;
         }
     }
-    flush_stats(stats, nrays & 0xffffu, nrays >> 16, nodes, prims);
-    if (lane == 0 && iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
+    if (lane == 0) {
+        if (ncl_w) atomicAdd(&stats->closest, (unsigned long long)ncl_w);
+        if (nsh_w) atomicAdd(&stats->shadow, (unsigned long long)nsh_w);
+        if (nodes_w) atomicAdd(&stats->nodes, (unsigned long long)nodes_w);
+        if (prims_w) atomicAdd(&stats->prims, (unsigned long long)prims_w);
+        if (iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
+    }
 #undef SPILL
 #undef STK
 }
