@@ -397,7 +397,7 @@ pt_status pt_render_range_accum(pt_scene* scene, int tile_offset, int tile_strid
                                 int sample_begin, int sample_end, float* accum_out,
                                 pt_stats* stats);
 
-/* Number of in-flight paths per wavefront batch (default 96M; 8M for the
+/* Number of in-flight paths per wavefront batch (default 96M; 32M for the
  * hero integrators).  Memory for path state is ~230 bytes per slot (~1.2 KB
  * for the hero integrators).  Batches beyond the 32-bit path-state indexing
  * limit (~252M slots; ~70M for hero scenes) are PT_ERR_INVALID_ARG. */

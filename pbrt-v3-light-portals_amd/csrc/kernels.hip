@@ -1846,7 +1846,7 @@ template <int kFt>
 constexpr bool kShadeAhead = false;
 #else
 template <int kFt>
-constexpr bool kShadeAhead = Ft<kFt>::mis && kFt != kFtAll;  // kFtAll: 228 -> 256 VGPRs, one wave
+constexpr bool kShadeAhead = Ft<kFt>::mis && !(Ft<kFt>::micro && Ft<kFt>::spec);  // two-lobe sets: 256 VGPRs, one wave
 #endif
 template <int kFt, bool kTab, bool kLean = false, bool kAb = false, bool kAhead = false>
 __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,

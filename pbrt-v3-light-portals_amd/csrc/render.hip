@@ -365,7 +365,7 @@ static ShadeKernel shade_kernel_ft(int variant, bool ab) {
     }
 }
 // Instantiated feature sets: all-matte, + infinite light, + spheres, + both,
-// everything.  Other combinations take the full kernel.
+// both BSDF kinds + infinite light without spheres, everything.  Other combinations take the full kernel.
 // ab: the build that counts the algorithmic path-state bytes (pt_set_count_bytes)
 static ShadeKernel shade_kernel(int variant, int features, bool ab = false) {
     if (features == kFtPortalOnly) return shade_kernel_ft<kFtPortalOnly>(variant, ab);  // matte, portal lights only
@@ -374,6 +374,8 @@ static ShadeKernel shade_kernel(int variant, int features, bool ab = false) {
         case kFtInfinite: return shade_kernel_ft<kFtInfinite>(variant, ab);
         case kFtSphere: return shade_kernel_ft<kFtSphere>(variant, ab);
         case kFtInfinite | kFtSphere: return shade_kernel_ft<kFtInfinite | kFtSphere>(variant, ab);
+        case kFtMicro | kFtSpecular | kFtInfinite:  // the dielectric Cornell box (C3): no sphere code
+            return shade_kernel_ft<kFtMicro | kFtSpecular | kFtInfinite>(variant, ab);
         default: return shade_kernel_ft<kFtAll>(variant, ab);
     }
 }
@@ -1226,7 +1228,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     };
     std::vector<Group> groups;
     // 96 M camera samples (C2: 64 M 877, 96 M 897, 128 M 896, 160 M 896 Msamples/s, same box)
-    size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)8 << 20 : (size_t)96 << 20);
+    // default batches: 96 M camera samples, 32 M for the hero integrators (1.2 KB of path state per slot:
+    // 38 GB per pipeline; C3h 8 / 16 / 32 / 64 M: 107.0 / 109.1 / 110.1 / 110.3 Msamples/s)
+    size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)32 << 20 : (size_t)96 << 20);
     {   // a render of only a few batches (one rank's shard of a multi-GPU frame) is split into equal batches, a
         // multiple of the pipelines, so the pipelines finish together instead of one running a short remainder
         // batch alone (PT_BATCH_EQUAL=<max batches>, 0 = off)

@@ -29,6 +29,9 @@ PT_SHADE_FT(kFtSphere)
 #if !defined(PT_FT) || PT_FT == 12
 PT_SHADE_FT(kFtInfinite | kFtSphere)
 #endif
+#if !defined(PT_FT) || PT_FT == 7
+PT_SHADE_FT(kFtMicro | kFtSpecular | kFtInfinite)
+#endif
 #if !defined(PT_FT) || PT_FT == 15
 PT_SHADE_FT(kFtAll)
 #endif
