@@ -293,12 +293,15 @@ SHADE_VARIANTS = [
 ]
 
 
-@pytest.mark.parametrize("scene", ["portal_cornell.pbrt", "portal_room.pbrt", "lamp/lamp.pbrt"])
+@pytest.mark.parametrize("scene", ["portal_cornell.pbrt", "portal_room.pbrt", "lamp/lamp.pbrt",
+                                   "cornell_dielectric.pbrt"])
 @pytest.mark.parametrize("env", SHADE_VARIANTS, ids=lambda e: "-".join("%s=%s" % kv for kv in e.items()))
 def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
     """Every shading build PT_SHADE_VARIANT can select, on a portal-only scene
-    (C2), a portal + infinite-light MIS scene (C4) and the reference's lamp
-    scene (MIS over a diffuse aaplane + portal light), renders the oracle's
+    (C2), a portal + infinite-light MIS scene (C4), the reference's lamp
+    scene (MIS over a diffuse aaplane + portal light) and the dielectric
+    Cornell box (C3: smooth and rough dispersive glass + infinite light, the
+    kFtMicro | kFtSpecular | kFtInfinite instantiation), renders the oracle's
     image bit for bit.  PT_SHADE_TAB=0 leaves no LDS room for the scene tables:
     variants 3 / 5 then fall back to k_shade instead of copying past the
     launch's LDS."""
@@ -309,7 +312,7 @@ def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
     hs, sc = _scene(path)
     if env == {"PT_SHADE_TAB": "0"}:
         assert sc.kernel_names()[1] == {"portal_cornell.pbrt": "k_shade_w3h", "portal_room.pbrt": "k_shade",
-                                        "lamp/lamp.pbrt": "k_shade_dl"}[scene]
+                                        "lamp/lamp.pbrt": "k_shade_dl", "cornell_dielectric.pbrt": "k_shade"}[scene]
     got, gst = sc.render()
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
