@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 10
+#define PT_ABI_VERSION 11
 
 typedef enum pt_status {
     PT_OK = 0,
@@ -292,6 +292,16 @@ typedef struct pt_stats {
                                   hero_path / hero_path_mis shading kernels always count (a 2-wave
                                   build either way: the counter register costs them no occupancy) */
     double reduce_ms;          /* pt_render_frame_dist: the ncclReduce of the film (HIP events on the stream) */
+    /* ABI 11: the 4-wide traversal (k_trace_w, LDS-resident scenes without spheres).  It returns the
+       reference's hits but not its visit order, so with trace_wide set node_visits / prim_tests count only
+       the rays it handed back to the binary traversal (retraced_rays: near ties within 2^-15 of the closest
+       t, hits at t <= 0, directions with a zero component); the reference's counters come from a render with
+       pt_set_count_bytes on, which traverses in the reference's order throughout. */
+    uint64_t retraced_rays;
+    uint64_t wide_node_visits; /* 4-wide node visits (112 B each) */
+    uint64_t wide_prim_tests;  /* primitive tests of the wide traversal */
+    int32_t trace_wide;        /* 1: this render traversed with k_trace_w */
+    int32_t reserved;
 } pt_stats;
 
 /* ---- host scene loader (.pbrt subset) ---- */
@@ -411,7 +421,10 @@ pt_status pt_set_pipelines(pt_scene* scene, int32_t pipelines);
 /* Count the shading kernel's algorithmic path-state bytes (pt_stats.shade_bytes)
  * in the renders that follow (default off: the count costs the 3-waves-per-SIMD
  * shading build a register, so it runs a separate instantiation).  Applies to
- * the path / mypath integrators; the hero integrators always count. */
+ * the path / mypath integrators; the hero integrators always count.  It is the
+ * counting frame's switch as a whole: with it on, every traversal runs the
+ * binary kernels in the reference's visit order (no k_trace_w), so the render's
+ * node_visits / prim_tests are the reference's counters. */
 pt_status pt_set_count_bytes(pt_scene* scene, int32_t on);
 
 /* Read back a setting of a device scene (what the environment overrides and
@@ -425,7 +438,7 @@ enum pt_scene_key {
     PT_Q_TRACE_SPILL = 3,      /* 1 when traversal stacks spill past the LDS rows (deep BVHs) */
     PT_Q_FEATURES = 4,         /* scene-feature set the shading kernel is instantiated for */
     PT_Q_TRACE_KERNEL = 5,     /* traversal kernel of a render: 0 k_trace, 1 k_trace_pt, 2 k_trace_nb, 3 k_trace_lds,
-                                  5 k_trace_oct */
+                                  5 k_trace_oct, 6 k_trace_w (+ k_trace_lds over its retrace queue) */
     PT_Q_SHADE_KERNEL = 6      /* shading kernel: 0 k_shade, 3 k_shade_w3, 4 k_shade_w3h, 5 k_shade_tab, 6 k_shade_dl,
                                   7 / 8 / 9 k_shade_hero / _w2 / _w4 */
 };
@@ -475,6 +488,10 @@ pt_status pt_debug_trace(pt_scene* scene, int n, const float* rays7, int any, in
  * the batch, the reference's BVHAccel counters (bvh.cpp:659-770). */
 pt_status pt_debug_trace_frame(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim,
                                uint64_t* counters);
+/* The same batch with the traversal's full counters (closest / shadow rays, node visits, primitive tests,
+ * and for k_trace_w its wide-node visits, primitive tests and retraced rays) in *stats. */
+pt_status pt_debug_trace_frame_ex(pt_scene* scene, int n, const float* rays7, int any, int32_t* out_prim,
+                                  pt_stats* stats);
 /* BSDF::f / Pdf / Sample_f of scene material `material` in the local shading
  * frame (n = (0,0,1)): per record in8 = wo[3], wi[3], u0, u1 and
  * out8 = f[3], pdf, sampled wi[3], sampled pdf (f is the sampled f when wi

@@ -5,9 +5,14 @@ directory first; nothing is written under the reference).
 
 Each edit inserts one-line read accessors into a class of the reference's
 headers -- the members the reference keeps private that GpuPathIntegrator
-(integration/gpupath.cpp) reads -- plus the two declarations the binding needs
-moved or kept: struct LinearBVHNode (defined in bvh.cpp:95-104) into bvh.h, and
-the BVH's node count (bvh.cpp:199, a local of the constructor) as a member.
+(integration/gpupath.cpp) reads.  The patch edits headers only and adds no
+state a .cpp file would have to set: the binding reads the BVH through
+BVHAccel::nodes (a pointer to the still-incomplete LinearBVHNode of bvh.h:52,
+whose 32-byte layout bvh.cpp:95-104 the binding mirrors and counts by walking
+the tree from node 0), and the constant radiance of an InfiniteAreaLight from
+its own Lmap (the 1x1 MIPMap infinite.cpp:43-61 builds).  The one member it
+adds, Sphere::phiMaxDegrees, is set in the constructor's init list, which
+sphere.h holds.
 The same getters appear, marked PATCH, in the stub mirror
 integration/pbrt_stub/stub_pbrt.h; tests/test_gpupath_reference_headers.py
 checks that the two name the same accessors.
@@ -31,8 +36,7 @@ PATCH = [
     ("accelerators/bvh.h", "BVHAccel", [
         "const std::vector<std::shared_ptr<Primitive>> &GetPrimitives() const { return primitives; }",
         "const LinearBVHNode *GetNodes() const { return nodes; }",
-        "int TotalNodes() const { return totalNodes; }",
-    ], ["int totalNodes = 0;  // the constructor's local (bvh.cpp:199) kept"], []),
+    ], [], []),
     ("core/primitive.h", "GeometricPrimitive", [
         "const Shape *GetShape() const { return shape.get(); }",
     ], [], []),
@@ -96,23 +100,9 @@ PATCH = [
     ], [], []),
     ("lights/infinite.h", "InfiniteAreaLight", [
         "const Transform &GetLightToWorld() const { return LightToWorld; }",
-        "const Spectrum *ConstantRadiance() const { return constantTexel.get(); }",
-    ], ["std::unique_ptr<Spectrum> constantTexel;  // set by the constructor (infinite.cpp:43-61) when texmap is empty"],
-        []),
+        "const MIPMap<RGBSpectrum> *GetLmap() const { return Lmap.get(); }",
+    ], [], []),
 ]
-
-# LinearBVHNode as bvh.cpp:95-104 lays it out (32 bytes), declared in bvh.h in place of the forward declaration
-LINEAR_BVH_NODE = """struct LinearBVHNode {
-    Bounds3f bounds;
-    union {
-        int primitivesOffset;   // leaf
-        int secondChildOffset;  // interior
-    };
-    uint16_t nPrimitives;  // 0 -> interior node
-    uint8_t axis;          // interior node: xyz
-    uint8_t pad[1];        // ensure 32 byte total size
-};"""
-
 
 def getter_names(patch=PATCH):
     """{class: sorted accessor names} of the patch."""
@@ -151,10 +141,6 @@ def apply(src_root):
             raise ValueError("%s: %s has no public: label" % (rel, cls))
         ins = "".join("\n    %s  // PATCH" % g for g in getters)
         text = text[:lab.end()] + ins + text[lab.end():]
-        if rel == "accelerators/bvh.h":
-            if "struct LinearBVHNode;" not in text:
-                raise ValueError("bvh.h: forward declaration of LinearBVHNode not found")
-            text = text.replace("struct LinearBVHNode;", LINEAR_BVH_NODE + "  // PATCH: moved from bvh.cpp", 1)
         open(path, "w").write(text)
 
 

@@ -306,11 +306,14 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
             mi.m[0][3] = -p.x; mi.m[1][3] = -p.y; mi.m[2][3] = -p.z;
             to_pt(Transform(m, mi), &l.light_to_world);
         } else if (const auto* il = dynamic_cast<const InfiniteAreaLight*>(lp.get())) {
-            const Spectrum* Lc = il->ConstantRadiance();  // infinite.cpp:43-61, a 1x1 Lmap
-            if (!Lc) return fail("gpupath: infinite light with an image map (only a constant radiance is flattened)");
+            // a constant radiance is the 1x1 Lmap infinite.cpp:43-61 builds without "mapname" (L itself); any
+            // 1x1 map is constant, a larger image map is not flattened
+            const MIPMap<RGBSpectrum>* lm = il->GetLmap();
+            if (!lm || lm->Width() != 1 || lm->Height() != 1)
+                return fail("gpupath: infinite light with an image map (only a constant radiance is flattened)");
             l.kind = PT_LIGHT_INFINITE;
             l.shape = -1;
-            Lc->ToRGB(l.L);
+            lm->Texel(0, 0, 0).ToRGB(l.L);
             to_pt(il->GetLightToWorld(), &l.light_to_world);
         } else
             return fail("gpupath: unsupported light (diffuse area, portal, point and constant infinite lights)");
@@ -318,9 +321,31 @@ bool FlattenScene(const Scene& scene, const GpuRenderSettings& settings, GpuFlat
     }
 
     // ---- the reference's flattened BVH ----
-    const int nn = bvh->TotalNodes();
+    // BVHAccel::nodes points at LinearBVHNode records (bvh.cpp:95-104: Bounds3f, primitivesOffset /
+    // secondChildOffset, nPrimitives, axis, pad -- 32 bytes, which bvh.h only forward-declares): the node count
+    // (bvh.cpp:199, a local of the constructor) is 1 + the largest index the depth-first layout reaches from
+    // node 0, found by walking it; no primitives: no nodes (bvh.cpp:190)
+    const unsigned char* raw = reinterpret_cast<const unsigned char*>(bvh->GetNodes());
+    int nn = 0;
+    if (raw && !bvh->GetPrimitives().empty()) {
+        auto field = [&](int i, int off, int bytes) {
+            int32_t v = 0;
+            std::memcpy(&v, raw + (size_t)i * 32 + off, (size_t)bytes);
+            return v;
+        };
+        std::vector<int> todo{0};
+        while (!todo.empty()) {
+            const int i = todo.back();
+            todo.pop_back();
+            nn = std::max(nn, i + 1);
+            if ((field(i, 28, 2) & 0xffff) == 0) {  // nPrimitives == 0: interior, children i + 1 and offset
+                todo.push_back(i + 1);
+                todo.push_back(field(i, 24, 4));
+            }
+        }
+    }
     f->bvh.resize((size_t)nn * 32);
-    std::memcpy(f->bvh.data(), bvh->GetNodes(), f->bvh.size());
+    if (nn) std::memcpy(f->bvh.data(), raw, f->bvh.size());
 
     pt_scene_desc& d = f->desc;
     std::memset(&d, 0, sizeof d);

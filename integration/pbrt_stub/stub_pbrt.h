@@ -410,19 +410,32 @@ class PointLight : public Light {
     const Spectrum I;
 };
 
-// lights/infinite.h:52-76 with a constant radiance (no "mapname"): the 1x1
-// Lmap texel L * scale (infinite.cpp:43-61)
+// core/mipmap.h: the queries the binding makes of an InfiniteAreaLight's Lmap
+template <typename T>
+class MIPMap {
+  public:
+    MIPMap(int w, int h, std::vector<T> texels) : w(w), h(h), texels(std::move(texels)) {}
+    int Width() const { return w; }
+    int Height() const { return h; }
+    const T& Texel(int level, int s, int t) const { (void)level; return texels[(size_t)t * w + s]; }
+  private:
+    int w, h;
+    std::vector<T> texels;
+};
+
+// lights/infinite.h:52-76; without "mapname" the constructor builds a 1x1 Lmap
+// holding L (infinite.cpp:43-61), as this one does
 class InfiniteAreaLight : public Light {
   public:
     InfiniteAreaLight(const Transform& LightToWorld, const Spectrum& L, int nSamples)
-        : Light(/* Infinite */ 8, nSamples), LightToWorld(LightToWorld), texel(L) {}
-    // PATCH: LightToWorld (light.h protected member) and the constant texel
-    // (nullptr return for an image map, which the binding refuses)
+        : Light(/* Infinite */ 8, nSamples), LightToWorld(LightToWorld),
+          Lmap(new MIPMap<RGBSpectrum>(1, 1, std::vector<RGBSpectrum>{L})) {}
+    // PATCH: LightToWorld (light.h protected member) and Lmap
     const Transform& GetLightToWorld() const { return LightToWorld; }
-    const Spectrum* ConstantRadiance() const { return &texel; }
+    const MIPMap<RGBSpectrum>* GetLmap() const { return Lmap.get(); }
   private:
     const Transform LightToWorld;
-    const Spectrum texel;
+    std::unique_ptr<MIPMap<RGBSpectrum>> Lmap;
 };
 
 // lights/portal_arealight.h
@@ -457,8 +470,9 @@ class GeometricPrimitive : public Primitive {
     std::shared_ptr<AreaLight> areaLight;
 };
 
-// accelerators/bvh.{h,cpp}: LinearBVHNode (bvh.cpp:95-104, moved to bvh.h by
-// the PATCH) and the flattened tree
+// accelerators/bvh.{h,cpp}: LinearBVHNode (bvh.cpp:95-104; the stub's test
+// driver fills records of it, the binding only sees the pointer) and the
+// flattened tree
 struct Bounds3f { Point3f pMin, pMax; };
 struct LinearBVHNode {
     Bounds3f bounds;
@@ -477,17 +491,14 @@ class BVHAccel : public Aggregate {
     // (BVHAccel::BVHAccel, bvh.cpp:186-236) handed in by the test driver
     BVHAccel(std::vector<std::shared_ptr<Primitive>> orderedPrims, std::vector<LinearBVHNode> flat)
         : primitives(std::move(orderedPrims)), flat(std::move(flat)) {
-        nodes = this->flat.data();
-        totalNodes = (int)this->flat.size();
+        nodes = this->flat.empty() ? nullptr : this->flat.data();
     }
     const std::vector<std::shared_ptr<Primitive>>& GetPrimitives() const { return primitives; }  // PATCH
     const LinearBVHNode* GetNodes() const { return nodes; }                                       // PATCH
-    int TotalNodes() const { return totalNodes; }  // PATCH (bvh.cpp:199's local kept as a member)
   private:
     std::vector<std::shared_ptr<Primitive>> primitives;
     std::vector<LinearBVHNode> flat;
     LinearBVHNode* nodes = nullptr;
-    int totalNodes = 0;
 };
 
 // core/scene.h:50-80

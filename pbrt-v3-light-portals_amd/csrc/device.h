@@ -98,6 +98,10 @@ struct DevScene {
     const float4* prims;
     int n_nodes;
     int n_prims;
+    // the same tree collapsed to 4-wide nodes (render.hip build_wide): 7 x float4 per node, k_trace_w
+    const float4* wnodes;
+    int n_wnodes;
+    float wide_scale;  // largest |coordinate| of the root bounds (k_trace_w's absolute tie margin)
     const pt_triangle* tris;
     const float* P;
     const float* N;
@@ -281,6 +285,9 @@ struct DevStats {
     unsigned long long lane_iters;  // k_trace_pt: lane-iterations executed (SIMD slots)
     unsigned long long lane_steps;  // k_trace_pt: node visits + primitive tests performed
     unsigned long long shade_bytes;  // k_shade (path integrator): algorithmic path-state bytes moved
+    unsigned long long wnodes;       // k_trace_w: wide-node visits (7 x 16 B each)
+    unsigned long long wprims;       // k_trace_w: primitive tests
+    unsigned long long retraced;     // k_trace_w: rays handed to the binary traversal (near ties, infinite 1/d)
 };
 
 }  // namespace pt

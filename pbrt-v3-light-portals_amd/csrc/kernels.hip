@@ -1182,6 +1182,356 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
 #endif
 
 // ----------------------------------------------------------------------------
+// k_trace_w: LDS-resident scenes traversed over a 4-wide BVH (round 6).
+//
+// The host collapses the reference's binary LinearBVHNode tree (bvh.cpp:640-658)
+// into nodes of up to four children (render.hip build_wide): a child is a binary
+// node of the original tree with its exact bounds -- an interior one becomes
+// another wide node, a leaf keeps its primitive range.  A node step loads the
+// four child boxes (7 x ds_read_b128), tests all four with the reference's box
+// test (Bounds3::IntersectP, geometry.h:1584-1606, the near / far planes picked
+// by address from the ray's direction signs), pushes the hit children farthest
+// first and continues at the nearest: about three dependent LDS round trips per
+// C2 ray instead of the binary walk's ~15.
+//
+// Same answers as BVHAccel::Intersect / IntersectP (bvh.cpp:662-738):
+//  * any-hit: the box test is monotone in the box (IEEE rounding is monotone,
+//    a parent's bounds contain its children's), so a primitive's leaf box passes
+//    only if every binary ancestor's does, and each leaf box is tested exactly:
+//    the primitives reached are the reference's and occlusion is order-free;
+//  * closest hit: the reference keeps the LAST accepted primitive, accepted
+//    against a tMax that shrinks in its visit order (Triangle::Intersect's
+//    scaled test, triangle.cpp:259-261; AAPlaneShape's `t < tMax` in the plane's
+//    object space, whose origin the Transform moved forward by its error bound,
+//    transform.h:303-316, plane.cpp:15-55), and culls boxes against it.  Every
+//    such t carries rounding errors of a few ulps of t plus absolute errors of
+//    order 100 eps x the coordinates involved (pbrt's own deltaT bound,
+//    triangle.cpp:362-385, the transformed origin's shift).  So here primitives
+//    are accepted -- and boxes culled -- against T = tBest + |tBest| 2^-17 + 2A,
+//    with A = 2^-10 (the scene's largest |coordinate| + the origin's), the
+//    smallest t wins and every other accepted t goes to t2.  When no other
+//    primitive is accepted within W = tBest + |tBest| 2^-18 + A, those margins
+//    are far beyond the error bounds and the winner is the only primitive the
+//    reference can keep whatever its order; otherwise -- a near tie, a hit at
+//    t <= 0 (aaplane: no t > 0 test), a NaN t, or a ray with an infinite 1/d
+//    component (NaN slabs) -- the ray goes to a retrace queue that the binary
+//    k_trace_lds traverses in the reference's order right after this launch.
+//    Hits are therefore the reference's, bit for bit; its node / primitive
+//    counters are not produced (the binary build runs for the counting frame,
+//    pt_set_count_bytes).
+//
+// Wide node image (112 B, 16-B aligned): {lo.x of children 0-3} {hi.x} {lo.y}
+// {hi.y} {lo.z} {hi.z} {child words}; a child word is 0x80000000 | the LDS byte
+// address of a wide node, or first primitive | count << 24 for a leaf; unused
+// slots have inverted bounds (+inf / -inf: never hit) and word 0.
+// ----------------------------------------------------------------------------
+// the acceptance / culling bound T and the tie window W around the best t (a: the ray's absolute margin A)
+__device__ __forceinline__ float wide_accept(float t, float a) { return t + fabsf(t) * (1.0f / 131072.0f) + 2 * a; }
+__device__ __forceinline__ float wide_tie(float t, float a) { return t + fabsf(t) * (1.0f / 262144.0f) + a; }
+
+// the wide node at cur (its six plane quads picked by the ray's direction signs: near x at cur + ax, far x at
+// cur + 16 - ax, ...) and the stack's top entry, one wait
+__device__ __forceinline__ void lds_wnode_top(uint32_t cur, uint32_t axyz, uint32_t sp, float4* nx, float4* fx,
+                                              float4* ny, float4* fy, float4* nz, float4* fz, uint4* wd,
+                                              uint32_t* top) {
+    const uint32_t c16 = cur + 16u;
+    const uint32_t ax = axyz & 0xffu, ay = (axyz >> 8) & 0xffu, az = axyz >> 16;
+    float4 a, b, c, d, e, f;
+    uint4 g;
+    uint32_t t;
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %9\n\t"
+        "ds_read_b128 %2, %10 offset:32\n\t"
+        "ds_read_b128 %3, %11 offset:32\n\t"
+        "ds_read_b128 %4, %12 offset:64\n\t"
+        "ds_read_b128 %5, %13 offset:64\n\t"
+        "ds_read_b128 %6, %14 offset:96\n\t"
+        "ds_read_b32 %7, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "=&v"(e), "=&v"(f), "=&v"(g), "=&v"(t)
+        : "v"(cur + ax), "v"(c16 - ax), "v"(cur + ay), "v"(c16 - ay), "v"(cur + az), "v"(c16 - az), "v"(cur),
+          "v"(sp)
+        : "memory");
+    *nx = a; *fx = b; *ny = c; *fy = d; *nz = e; *fz = f; *wd = g; *top = t;
+}
+// three entries above the top (the node step's pushes; rows past the new top are dead)
+__device__ __forceinline__ void lds_push3(uint32_t sp, uint32_t a, uint32_t b, uint32_t c) {
+    asm volatile("ds_write_b32 %0, %1 offset:512\n\tds_write_b32 %0, %2 offset:1024\n\tds_write_b32 %0, %3 offset:1536"
+                 : : "v"(sp), "v"(a), "v"(b), "v"(c) : "memory");
+}
+
+// The reference's box test (box_hit_mm without its NaN-slab term: a ray with an infinite 1/d component is
+// retraced by the binary kernel) for two children at once: p*/q* their near / far planes, packed.
+struct WideHit2 {
+    pt_f2 f0;
+    bool h0, h1;
+};
+// ix / iy / iz: 1/d splatted to both halves (kept per ray: built per step, the splats went through scratch)
+__device__ __forceinline__ WideHit2 wide_box2(pt_f2 nx, pt_f2 fx, pt_f2 ny, pt_f2 fy, pt_f2 nz, pt_f2 fz, pt_f2 ox,
+                                              pt_f2 oy, pt_f2 oz, pt_f2 ix, pt_f2 iy, pt_f2 iz, float tc) {
+    const float kx = 1 + 2 * gammaf(3);
+    const pt_f2 tx0 = (nx - ox) * ix, tx1 = ((fx - ox) * ix) * kx;
+    const pt_f2 ty0 = (ny - oy) * iy, ty1 = ((fy - oy) * iy) * kx;
+    const pt_f2 tz0 = (nz - oz) * iz, tz1 = ((fz - oz) * iz) * kx;
+    WideHit2 r;
+    r.f0.x = __builtin_fmaxf(__builtin_fmaxf(tx0.x, ty0.x), tz0.x);
+    r.f0.y = __builtin_fmaxf(__builtin_fmaxf(tx0.y, ty0.y), tz0.y);
+    const float f1a = __builtin_fminf(__builtin_fminf(tx1.x, ty1.x), tz1.x);
+    const float f1b = __builtin_fminf(__builtin_fminf(tx1.y, ty1.y), tz1.y);
+    r.h0 = !(r.f0.x > f1a) & (r.f0.x < tc) & (f1a > 0);
+    r.h1 = !(r.f0.y > f1b) & (r.f0.y < tc) & (f1b > 0);
+    return r;
+}
+
+#ifndef PT_WNODE_STEPS
+#define PT_WNODE_STEPS 2
+#endif
+constexpr int kWNodeSteps = PT_WNODE_STEPS;
+// 6 waves per SIMD (80 VGPRs, no scratch; the compiler's own choice is 82 = 5 waves, and 7 waves spill 40 B)
+#ifdef PT_TRACE_W_WAVES
+#define PT_TRACE_W_ATTR __attribute__((amdgpu_waves_per_eu(PT_TRACE_W_WAVES)))
+#else
+#define PT_TRACE_W_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#endif
+__global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScene sc, DevPaths ps,
+                                                                        const uint32_t* __restrict__ rq,
+                                                                        const uint32_t* __restrict__ rq_count,
+                                                                        uint32_t* fetch, int refill_min, int leaf_min,
+                                                                        uint32_t* retrace_q, uint32_t* retrace_n,
+                                                                        DevStats* stats)
+#ifdef PT_TU_TRACE
+{
+    extern __shared__ float4 lds_dyn[];
+    const int nw = 7 * sc.n_wnodes;
+    const int scene_f4 = nw + 3 * sc.n_prims;
+    const uint32_t node0 = (uint32_t)(uintptr_t)lds_dyn;  // wide nodes are named by their LDS byte address
+    for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
+        float4 v = i < nw ? sc.wnodes[i] : sc.prims[i - nw];
+        if (i < nw && i % 7 == 6) {  // child words: image offsets -> LDS addresses
+            uint32_t w[4] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+            for (int k = 0; k < 4; ++k)
+                if ((int)w[k] < 0) w[k] = 0x80000000u | (node0 + (w[k] & 0x7fffffffu));
+            v = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+        }
+        lds_dyn[i] = v;
+    }
+    __syncthreads();
+    const float4* bprims = lds_dyn + nw;
+    // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
+    const uint32_t sbase = (uint32_t)(uintptr_t)((uint32_t*)(lds_dyn + scene_f4) + threadIdx.x);
+    const uint32_t n = *rq_count;
+    const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
+    const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
+    const uint32_t lane = lane_id();
+    uint32_t nrays = 0, wnp = 0;  // nrays: closest + shadow << 16; wnp: wide nodes + prim tests << 16
+    unsigned long long iters_w = 0;
+    bool active = false, exhausted = false, drained = false, retr = false;
+    uint32_t qn = 0, qe = 0;
+    uint32_t ent = 0;  // the ray-queue entry: slot << 2 | kind
+    // the ray: its origin and 1/d splatted to both halves of a pair (the packed box tests' operands; .x the
+    // scalar), the bound T; the direction itself is reloaded only for analytic shapes (aaplane tests)
+    pt_f2 ox = {0, 0}, oy = {0, 0}, oz = {0, 0}, ix = {0, 0}, iy = {0, 0}, iz = {0, 0};
+    float tmx = 0;
+    TriShear sh{0, 0, 0, 0};
+    uint32_t axyz = 0, sp = sbase, cur = node0;  // axyz: the near planes' offsets per axis (bytes 0-2: 0 / 16)
+    float tBest = kInf, t2 = kInf;  // closest accepted t and the smallest other accepted t
+    int hitPrim = -1;
+    uint32_t lf = 0;  // the leaf being tested: next primitive | primitives left << 24 (a leaf child word)
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= rmin) {
+                if (qn >= qe && !drained) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(fetch, kTraceChunk);
+                    base = __builtin_amdgcn_readlane(base, 0);
+                    qn = base < n ? base : n;
+                    qe = base + kTraceChunk < n ? base + kTraceChunk : n;
+                    drained = base + kTraceChunk >= n;
+                }
+                const uint32_t take = qe - qn < nidle ? qe - qn : nidle;
+                const uint32_t k = lanes_below(idle);
+                const uint32_t i = qn + k;
+                qn += take;
+                if (drained && qn >= qe) exhausted = true;
+                if (!active && k < take) {
+                    const uint32_t e = rq[i];
+                    ent = e;
+                    const uint32_t slot = e >> 2, kind = e & 3u;
+                    const Ray ray = load_ray_trace(kind == kRayCont ? ps.ray : (kind == kRayB ? ps.rayB : ps.rayA),
+                                                   slot, kind == kRayShadow);
+                    ox = pt_f2{ray.o.x, ray.o.x};
+                    oy = pt_f2{ray.o.y, ray.o.y};
+                    oz = pt_f2{ray.o.z, ray.o.z};
+                    tmx = ray.tmax;
+                    const V3 inv = v3(1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z);
+                    ix = pt_f2{inv.x, inv.x};
+                    iy = pt_f2{inv.y, inv.y};
+                    iz = pt_f2{inv.z, inv.z};
+                    sh = tri_shear(ray.d);
+                    axyz = (inv.x < 0 ? 16u : 0u) | (inv.y < 0 ? 16u << 8 : 0u) | (inv.z < 0 ? 16u << 16 : 0u);
+                    // NaN slabs (0 * inf) only arise with an infinite 1/d component: the binary kernel's case
+                    retr = !(__builtin_fmaxf(__builtin_fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z)) < kInf);
+                    cur = node0; sp = sbase; hitPrim = -1; lf = 0;
+                    tBest = kInf; t2 = kInf;
+                    active = sc.n_wnodes > 0;  // empty scene: every ray misses
+                    if (!active) {
+                        if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = 0;
+                        else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = -1;
+                        else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = -1;
+                        else *hit_word(ps, slot, kHdHitB) = -1;
+                        nrays += kind == kRayShadow ? 0x10000u : 1u;
+                    }
+                }
+            }
+        }
+        const bool wantLeaf = active && lf >= (1u << 24);
+        const uint64_t mLeaf = __ballot(wantLeaf);
+        const uint64_t mNode = __ballot(active && !wantLeaf);
+        if ((mLeaf | mNode) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        const uint32_t nLeaf = (uint32_t)__popcll(mLeaf);
+        const bool leafStep = nLeaf > 0 && (mNode == 0 || nLeaf >= lmin);
+        ++iters_w;
+        bool done = false;
+        const bool shadow = (ent & 3u) == kRayShadow;
+        // the ray's absolute margin A (not kept: one register less)
+        const float amarg = (sc.wide_scale + __builtin_fmaxf(__builtin_fmaxf(fabsf(ox.x), fabsf(oy.x)), fabsf(oz.x))) *
+                            (1.0f / 1024.0f);
+        if (leafStep) {
+#pragma unroll
+            for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
+                if (!(active && !done && lf >= (1u << 24))) continue;
+                const int pi = (int)(lf & 0xffffffu);
+                lf += 1u - (1u << 24);
+                wnp += 0x10000u;
+                const float4 r0 = bprims[3 * pi];
+                const float4 r1 = bprims[3 * pi + 1];
+                const float4 r2 = bprims[3 * pi + 2];
+                const uint32_t fl = __float_as_uint(r0.w);
+                float t = 0;
+                bool ok;
+                if (fl & kPrimAnalytic) {
+                    const uint32_t kd = ent & 3u;
+                    Ray ray = load_ray_trace(kd == kRayCont ? ps.ray : (kd == kRayB ? ps.rayB : ps.rayA), ent >> 2,
+                                             false);
+                    ray.tmax = tmx;
+                    ok = shape_test<false>(sc, fl, __float_as_int(r1.w), ray, &t);
+                } else {
+                    const Ray ray{v3(ox.x, oy.x, oz.x), v3(0, 0, 0), tmx};  // tri_hit reads o and tMax (+ the shear)
+                    ok = tri_hit(v3(r0.x, r0.y, r0.z), v3(r1.x, r1.y, r1.z), v3(r2.x, r2.y, r2.z), ray, sh, &t);
+                    ok &= shadow | !(fl & kPrimDegenerate);
+                }
+                if (shadow) {
+                    hitPrim = ok ? pi : hitPrim;
+                    done = ok;
+                } else if (ok) {
+                    const bool better = !(t >= tBest);  // a NaN t is kept (and retraced below)
+                    t2 = __builtin_fminf(t2, better ? tBest : t);
+                    tBest = better ? t : tBest;
+                    hitPrim = better ? pi : hitPrim;
+                    tmx = better ? wide_accept(t, amarg) : tmx;
+                }
+                if (!done && lf < (1u << 24)) {  // the leaf is finished: pop
+                    const bool empty = sp == sbase;
+                    done = empty;
+                    if (!empty) {
+                        const uint32_t w = (uint32_t)lds_top(sp);
+                        sp -= 512;
+                        const bool inner = (int)w < 0;
+                        cur = inner ? (w & 0x7fffffffu) : cur;
+                        lf = inner ? 0u : w;
+                    }
+                }
+            }
+        } else {
+            const bool nm0 = active & (lf < (1u << 24));
+            bool nm = nm0;
+#pragma unroll
+            for (int u = 0; u < kWNodeSteps; ++u) {
+                if (!nm) continue;
+                ++wnp;
+                float4 nx, fx, ny, fy, nz, fz;
+                uint4 wd;
+                uint32_t top;
+                lds_wnode_top(cur, axyz, sp, &nx, &fx, &ny, &fy, &nz, &fz, &wd, &top);
+                const float tc = tmx;
+                const WideHit2 h01 = wide_box2(pt_f2{nx.x, nx.y}, pt_f2{fx.x, fx.y}, pt_f2{ny.x, ny.y},
+                                               pt_f2{fy.x, fy.y}, pt_f2{nz.x, nz.y}, pt_f2{fz.x, fz.y}, ox, oy, oz, ix, iy, iz,
+                                               tc);
+                const WideHit2 h23 = wide_box2(pt_f2{nx.z, nx.w}, pt_f2{fx.z, fx.w}, pt_f2{ny.z, ny.w},
+                                               pt_f2{fy.z, fy.w}, pt_f2{nz.z, nz.w}, pt_f2{fz.z, fz.w}, ox, oy, oz, ix, iy, iz,
+                                               tc);
+                // sort keys: a hit child's entry distance (> -inf), a missed one -inf; descending, so the hits
+                // come first, farthest to nearest
+                const float kHitMin = -3.40282347e38f;
+                float k0 = h01.h0 ? __builtin_fmaxf(h01.f0.x, kHitMin) : -kInf;
+                float k1 = h01.h1 ? __builtin_fmaxf(h01.f0.y, kHitMin) : -kInf;
+                float k2 = h23.h0 ? __builtin_fmaxf(h23.f0.x, kHitMin) : -kInf;
+                float k3 = h23.h1 ? __builtin_fmaxf(h23.f0.y, kHitMin) : -kInf;
+                uint32_t w0 = wd.x, w1 = wd.y, w2 = wd.z, w3 = wd.w;
+#define PT_WCAS(a, b)                                   \
+    {                                                   \
+        const bool s_ = k##a < k##b;                    \
+        const float ka_ = s_ ? k##b : k##a;             \
+        k##b = s_ ? k##a : k##b;                        \
+        k##a = ka_;                                     \
+        const uint32_t wa_ = s_ ? w##b : w##a;          \
+        w##b = s_ ? w##a : w##b;                        \
+        w##a = wa_;                                     \
+    }
+                PT_WCAS(0, 1) PT_WCAS(2, 3) PT_WCAS(0, 2) PT_WCAS(1, 3) PT_WCAS(1, 2)
+#undef PT_WCAS
+                const uint32_t nh = (uint32_t)h01.h0 + (uint32_t)h01.h1 + (uint32_t)h23.h0 + (uint32_t)h23.h1;
+                lds_push3(sp, w0, w1, w2);  // the hits but the nearest (rows past the new top are dead)
+                const bool empty = sp == sbase;
+                const bool pop = (nh == 0) & !empty;
+                const uint32_t nxt = nh == 0 ? top : (nh == 1 ? w0 : (nh == 2 ? w1 : (nh == 3 ? w2 : w3)));
+                sp = nh > 0 ? sp + 512u * (nh - 1u) : (pop ? sp - 512u : sp);
+                const bool go = (nh > 0) | pop;
+                const bool inner = go & ((int)nxt < 0);
+                const bool leaf = go & ((int)nxt >= 0);
+                nm = inner;
+                cur = inner ? (nxt & 0x7fffffffu) : cur;
+                lf = leaf ? nxt : lf;
+            }
+            done = nm0 & !nm & (lf < (1u << 24));  // left the BVH: a miss with an empty stack
+        }
+        if (done) {
+            const uint32_t slot = ent >> 2, kind = ent & 3u;
+            // closest hit: retrace near ties (another accepted t within W) and hits at t <= 0 / NaN
+            const bool tie = !shadow && hitPrim >= 0 && (!(tBest > 0) || t2 <= wide_tie(tBest, amarg));
+            if (retr || tie) {  // counted by the retrace launch (its own DevStats)
+                retrace_q[atomicAdd(retrace_n, 1u)] = ent;
+            } else {
+                if (kind == kRayShadow) *hit_word(ps, slot, kHdHitA) = hitPrim >= 0 ? 1 : 0;
+                else if (kind == kRayCont) *hit_word(ps, slot, kHdHit) = hitPrim;
+                else if (kind == kRayA) *hit_word(ps, slot, kHdHitA) = hitPrim;
+                else *hit_word(ps, slot, kHdHitB) = hitPrim;
+                nrays += kind == kRayShadow ? 0x10000u : 1u;
+            }
+            active = false;
+        }
+    }
+    flush_stats(stats, nrays & 0xffffu, nrays >> 16, 0, 0);
+    {
+        const unsigned long long a = wave_sum_u64(wnp & 0xffffu), b = wave_sum_u64(wnp >> 16);
+        if (lane == 0) {
+            if (a) atomicAdd(&stats->wnodes, a);
+            if (b) atomicAdd(&stats->wprims, b);
+            if (iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
+        }
+    }
+}
+#else
+;
+#endif
+
+// ----------------------------------------------------------------------------
 // Camera rays: GetCameraSample (sampler.cpp:46-53) + GenerateRayDifferential
 // (perspective.cpp:100-154) + CameraToWorld (transform.h:251-264)
 // ----------------------------------------------------------------------------

@@ -165,12 +165,14 @@ constexpr int kMaxPipes = 4;  // render_tiles pipelines (PT_PIPES)
 
 struct Work {
     DBuf<uint32_t> rq0, rq1, pq0, pq1, counts;
+    DBuf<uint32_t> rqr;  // k_trace_w: ray-queue entries handed to the binary traversal (counts[6])
     DBuf<uint4> head;   // DevPaths records (device.h)
     DBuf<float4> body;
     DBuf<float2> pfilm;
     DBuf<float> ray, rayA, rayB, nee, Lfin;
     DBuf<int> spill;
     DBuf<DevStats> stats;
+    DBuf<DevStats> stats_rt;  // the retrace launches after k_trace_w (their rays are the retraced_rays)
     DBuf<int> dli;                 // DirectLighting state (kDl*)
     DBuf<float> dlf, dlframe;
     DBuf<float> h_out60, h_outy, h_L60, h_beta60, h_nee60, h_hs;  // hero integrators: 60-bin state per slot
@@ -209,7 +211,7 @@ struct Work {
             dl_frames = frames;
         }
         if (n > cap) {
-            rq0.alloc(3 * n); rq1.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
+            rq0.alloc(3 * n); rq1.alloc(3 * n); rqr.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
             head.alloc(n); body.alloc(2 * n); pfilm.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
             rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); Lfin.alloc(3 * n);
             cap = n;
@@ -217,6 +219,7 @@ struct Work {
         spill.alloc(spill_threads * 64);  // k_trace_pt: 64 words per lane (entries past its LDS rows)
         counts.alloc(8);
         stats.alloc(1);
+        stats_rt.alloc(1);
     }
     DevPaths paths(int n) {
         DevPaths p{};
@@ -247,6 +250,7 @@ struct pt_scene {
     // stream of the scene was freed with the scene's own device current
     pt::DeviceRestore restore_dev;
     pt::DBuf<float4> nodes, prims;
+    pt::DBuf<float4> wnodes;  // the BVH collapsed to 4-wide nodes (build_wide; k_trace_w)
     pt::DBuf<pt_triangle> tris;
     pt::DBuf<float> P, N, S, UV, lfunc, lcdf, tri_area, perm_c0;
     pt::DBuf<pt::DevPlane> planes, pplanes;
@@ -288,6 +292,9 @@ struct pt_scene {
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     size_t oct_lds_bytes = 0;    // > 0: k_trace_oct (octant images of an LDS-sized BVH; opt-in PT_TRACE_OCT=1)
+    size_t wide_lds_bytes = 0;   // > 0: k_trace_w (4-wide BVH image + primitive records + stack; PT_TRACE_WIDE=0 disables)
+    int wide_rows = 0;           // k_trace_w LDS stack rows per lane (dummy row + deepest stack + 3 push rows)
+    int leaf_min_w = 32;         // k_trace_w: lanes parked at leaves that trigger a primitive-test step (PT_LEAF_MIN_W)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
@@ -1113,6 +1120,7 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
 // scene (pt_scene_query PT_Q_TRACE_KERNEL / PT_Q_SHADE_KERNEL; the bench names
 // the kernel its roofline is for).
 static int trace_kernel_id(const pt_scene* s) {
+    if (s->wide_lds_bytes && !s->count_bytes) return 6;
     if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean)
         return s->oct_lds_bytes ? 5 : 3;
     if (s->trace_persist == 2 && !s->trace_spill) return 2;
@@ -1131,6 +1139,17 @@ static int shade_kernel_id(const pt_scene* s) {
 static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
                          hipStream_t st) {
     const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+    if (s->wide_lds_bytes && !s->count_bytes) {
+        // k_trace_w over the queue, then the binary k_trace_lds over the rays it hands back (near ties,
+        // infinite 1/d): counts[6] their number, counts[7] that launch's fetch cursor
+        hipLaunchKernelGGL(k_trace_w, pg, dim3(kTraceBlock), s->wide_lds_bytes, st, s->dev, ps, rq, counts + 0,
+                           counts + 4, s->refill_min, s->leaf_min_w, w.rqr.p, counts + 6, w.stats.p);
+        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
+        const dim3 rg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * 2)));
+        hipLaunchKernelGGL(trace_lds_kernel(false), rg, dim3(kTraceBlock), lds, st, s->dev, ps, w.rqr.p, counts + 6,
+                           counts + 7, s->refill_min, s->leaf_min, w.stats_rt.p);
+        return;
+    }
     if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && s->oct_lds_bytes) {
         // k_trace_oct: eight octant images of the BVH + the primitive records + the stack, 4 blocks per CU
         const dim3 og(std::max(1, std::min(ceil_div(nrays, kOctBlock), s->num_cus * 4)));
@@ -1178,6 +1197,8 @@ __global__ void k_next_counts(uint32_t* c, volatile uint32_t* host) {
     c[3] = 0;
     c[4] = 0;
     c[5] = 0;
+    c[6] = 0;
+    c[7] = 0;
 }
 
 __global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
@@ -1187,12 +1208,30 @@ __global__ void k_set_counts(uint32_t* c, uint32_t rays, uint32_t paths) {
     c[3] = 0;
     c[4] = 0;
     c[5] = 0;
+    c[6] = 0;
+    c[7] = 0;
+}
+
+// A pipeline's counters: its kernels' and the retrace launches' (k_trace_w hands rays back to the binary
+// traversal; those count their rays, node visits and primitive tests, and are the retraced rays)
+static DevStats read_stats(const Work& w) {
+    DevStats d{}, r{};
+    HIPCHK(hipMemcpy(&d, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&r, w.stats_rt.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+    d.closest += r.closest;
+    d.shadow += r.shadow;
+    d.nodes += r.nodes;
+    d.prims += r.prims;
+    d.lane_iters += r.lane_iters;
+    d.retraced += r.closest + r.shadow;
+    return d;
 }
 
 struct RenderResult {
     DevStats st{};
     double render_ms = 0, trace_ms = 0, shade_ms = 0;
     uint64_t launches = 0, samples = 0, shade_launches = 0;
+    bool wide = false;  // traversed with k_trace_w (node / primitive counters: the retraced rays only)
 };
 
 // Render the given tiles into the device accumulation buffer d_accum
@@ -1212,6 +1251,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     std::vector<TileSpan> tiles;
     tile_pixels(fr, offset, stride, &pix, &tiles);
     RenderResult rr;
+    rr.wide = s->wide_lds_bytes && !s->count_bytes;
     const int npix = (int)pix.size();
     const int spp = s_end - s_begin;
     if (npix == 0 || spp == 0) return rr;
@@ -1299,6 +1339,7 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                  direct ? s->dev.dl_frames : 0, s->hero ? (int)max_slots : 0);
         if (!w.stream) HIPCHK(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
         HIPCHK(hipMemsetAsync(w.stats.p, 0, sizeof(DevStats), w.stream));
+        HIPCHK(hipMemsetAsync(w.stats_rt.p, 0, sizeof(DevStats), w.stream));
     }
     // the caller's stream has everything before this call (e.g. the film clear)
     {
@@ -1486,11 +1527,11 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
     rr.render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (auto& e : film_done) (void)hipEventDestroy(e);
     for (int k = 0; k < pipes; ++k) {
-        DevStats d{};
-        HIPCHK(hipMemcpy(&d, s->work[k].stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+        const DevStats d = read_stats(s->work[k]);
         rr.st.closest += d.closest; rr.st.shadow += d.shadow; rr.st.nodes += d.nodes; rr.st.prims += d.prims;
         rr.st.dim_overflow += d.dim_overflow; rr.st.lane_iters += d.lane_iters; rr.st.lane_steps += d.lane_steps;
         rr.st.shade_bytes += d.shade_bytes;
+        rr.st.wnodes += d.wnodes; rr.st.wprims += d.wprims; rr.st.retraced += d.retraced;
         rr.trace_ms += pt[k].trace_ms;
         rr.shade_ms += pt[k].shade_ms;
         rr.launches += pt[k].launches;
@@ -1569,6 +1610,11 @@ static void fill_stats(const RenderResult& r, pt_stats* st) {
     st->shade_launches = r.shade_launches;
     st->shade_bytes = r.st.shade_bytes;
     st->reduce_ms = 0;
+    st->retraced_rays = r.st.retraced;
+    st->wide_node_visits = r.st.wnodes;
+    st->wide_prim_tests = r.st.wprims;
+    st->trace_wide = r.wide ? 1 : 0;
+    st->reserved = 0;
 }
 
 template <class F>
@@ -1619,6 +1665,93 @@ static int bvh_stack_bound(const std::vector<LinearNode>& nodes) {
         todo.push_back({nodes[i].offset, d + 1});
     }
     return best;
+}
+
+// The binary BVH collapsed to 4-wide nodes for k_trace_w (kernels.hip): a wide node takes its binary
+// node's two children and opens the interior child of largest surface area until it holds four children
+// (or only leaves are left); every child is a node of the reference's tree with its exact bounds -- an
+// interior one becomes the next wide node, a leaf keeps its primitive range (bvh.cpp:640-658 layout).
+// Image per wide node (112 B): {lo.x of children 0-3} {hi.x} {lo.y} {hi.y} {lo.z} {hi.z} {child words};
+// child word = 0x80000000 | byte offset of a wide node in the image (the kernel adds the LDS base), or
+// first primitive | count << 24 for a leaf; unused slots: bounds +inf / -inf (never hit) and word 0.
+// *rows: LDS stack rows per lane -- the dummy row, the deepest stack a node can be visited at, and the three
+// rows the node step writes above its top.  Returns false when the tree does not fit the child-word encoding.
+static bool build_wide(const std::vector<LinearNode>& bn, std::vector<float4>* img, int* n_wide, int* rows) {
+    img->clear();
+    *n_wide = 0;
+    *rows = 0;
+    if (bn.empty()) return true;
+    for (const LinearNode& n : bn)
+        if (n.nprims > 127 || (n.nprims > 0 && (uint64_t)n.offset + n.nprims > (1u << 24))) return false;
+    auto area = [&](int i) {
+        const LinearNode& n = bn[i];
+        const double dx = (double)n.bmax[0] - n.bmin[0], dy = (double)n.bmax[1] - n.bmin[1],
+                     dz = (double)n.bmax[2] - n.bmin[2];
+        return dx * dy + dy * dz + dx * dz;
+    };
+    struct Wide { int bin[4], wid[4]; };  // children: binary node ids (-1 unused), wide ids of interior ones
+    std::vector<Wide> wn(1);
+    struct Todo { int bin, wide, depth; };
+    std::vector<Todo> todo{{0, 0, 0}};
+    int max_depth = 0;
+    std::vector<int> ch;
+    while (!todo.empty()) {
+        const Todo t = todo.back();
+        todo.pop_back();
+        ch.clear();
+        if (bn[t.bin].nprims > 0) ch.push_back(t.bin);  // a one-leaf tree
+        else { ch.push_back(t.bin + 1); ch.push_back(bn[t.bin].offset); }
+        while (ch.size() < 4) {
+            int best = -1;
+            for (int k = 0; k < (int)ch.size(); ++k)
+                if (bn[ch[k]].nprims == 0 && (best < 0 || area(ch[k]) > area(ch[best]))) best = k;
+            if (best < 0) break;
+            const int c = ch[best];
+            ch[best] = c + 1;
+            ch.push_back(bn[c].offset);
+        }
+        max_depth = std::max(max_depth, t.depth);
+        Wide w{{-1, -1, -1, -1}, {-1, -1, -1, -1}};
+        for (int k = 0; k < (int)ch.size(); ++k) {
+            w.bin[k] = ch[k];
+            if (bn[ch[k]].nprims == 0) {
+                w.wid[k] = (int)wn.size();
+                wn.push_back(Wide{});
+                // visited with up to (children - 1) entries pushed above the parent's stack
+                todo.push_back({ch[k], w.wid[k], t.depth + (int)ch.size() - 1});
+            }
+        }
+        wn[t.wide] = w;
+    }
+    const size_t nw = wn.size();
+    if (nw * 112u >= 0x80000000ull) return false;
+    img->assign(nw * 7, make_float4(0, 0, 0, 0));
+    for (size_t i = 0; i < nw; ++i) {
+        float lo[3][4], hi[3][4];
+        uint32_t word[4];
+        for (int k = 0; k < 4; ++k) {
+            const int c = wn[i].bin[k];
+            if (c < 0) {
+                for (int a = 0; a < 3; ++a) { lo[a][k] = INFINITY; hi[a][k] = -INFINITY; }
+                word[k] = 0;
+                continue;
+            }
+            const LinearNode& n = bn[c];
+            for (int a = 0; a < 3; ++a) { lo[a][k] = n.bmin[a]; hi[a][k] = n.bmax[a]; }
+            word[k] = n.nprims > 0 ? ((uint32_t)n.offset | ((uint32_t)n.nprims << 24))
+                                   : (0x80000000u | (uint32_t)(112 * wn[i].wid[k]));
+        }
+        float4* q = img->data() + 7 * i;
+        for (int a = 0; a < 3; ++a) {
+            q[2 * a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
+            q[2 * a + 1] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
+        }
+        q[6] = make_float4(__builtin_bit_cast(float, word[0]), __builtin_bit_cast(float, word[1]),
+                           __builtin_bit_cast(float, word[2]), __builtin_bit_cast(float, word[3]));
+    }
+    *n_wide = (int)nw;
+    *rows = max_depth + 4;
+    return true;
 }
 
 // One device's copy of the scene: build (or copy the BVH of bvh_src),
@@ -1693,10 +1826,34 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                                                                           : (size_t)prop.sharedMemPerMultiprocessor;
         s->oct_lds_bytes = (s->lds_scene_bytes && !s->trace_spill && 4 * oct <= cu_lds && t && t[0] == '1') ? oct : 0;
     }
+    {   // k_trace_w (4-wide BVH) for the scenes k_trace_lds traverses, without spheres (the sphere test's EFloat
+        // acceptance is left to the binary order); the binary kernel stays the retrace and counting traversal
+        const char* t = std::getenv("PT_TRACE_WIDE");
+        std::vector<float4> img;
+        int nw = 0, rows = 0;
+        if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && !s->oct_lds_bytes &&
+            !s->has_spheres && !(t && t[0] == '0') && build_wide(s->host_nodes, &img, &nw, &rows) && nw > 0) {
+            const size_t scene = (size_t)nw * 112 + (size_t)s->dev.n_prims * 48;
+            if (scene <= (size_t)kLdsSceneMax + 4096 && rows <= 64) {
+                s->wnodes.upload(img);
+                s->dev.wnodes = s->wnodes.p;
+                s->dev.n_wnodes = nw;
+                float sc_max = 0;
+                for (int k = 0; k < 3; ++k)
+                    sc_max = std::max({sc_max, std::fabs(s->host_nodes[0].bmin[k]), std::fabs(s->host_nodes[0].bmax[k])});
+                s->dev.wide_scale = sc_max;
+                s->wide_rows = rows;
+                s->wide_lds_bytes = scene + (size_t)rows * kTraceBlock * sizeof(uint32_t);
+            }
+        }
+        if (const char* l = std::getenv("PT_LEAF_MIN_W")) s->leaf_min_w = std::max(1, std::atoi(l));
+    }
     if (std::getenv("PT_TRACE_DEBUG"))
-        std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, trace kernel %s\n", s->stack_rows,
-                     s->trace_spill, s->lds_scene_bytes,
-                     s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean ? "k_trace_lds"
+        std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, wide %zu B (%d nodes, %d rows), "
+                     "trace kernel %s\n", s->stack_rows, s->trace_spill, s->lds_scene_bytes, s->wide_lds_bytes,
+                     s->dev.n_wnodes, s->wide_rows,
+                     s->wide_lds_bytes                                                             ? "k_trace_w"
+                     : s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean ? "k_trace_lds"
                      : s->trace_persist == 2 && !s->trace_spill                                    ? "k_trace_nb"
                      : s->trace_persist                                                            ? "k_trace_pt"
                                                                                                    : "k_trace");
@@ -1731,6 +1888,8 @@ static void add_stats(RenderResult* a, const RenderResult& b) {
     a->shade_ms += b.shade_ms;
     a->shade_launches += b.shade_launches;
     a->st.shade_bytes += b.st.shade_bytes;
+    a->st.wnodes += b.st.wnodes; a->st.wprims += b.st.wprims; a->st.retraced += b.st.retraced;
+    a->wide |= b.wide;
     a->render_ms = std::max(a->render_ms, b.render_ms);
 }
 
@@ -2189,9 +2348,20 @@ pt_status pt_debug_trace(pt_scene* s, int n, const float* rays7, int any, int32_
 
 pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, int32_t* out_prim,
                                uint64_t* counters) {
+    pt_stats st{};
+    const pt_status r = pt_debug_trace_frame_ex(s, n, rays7, any, out_prim, &st);
+    if (r == PT_OK && counters) {
+        counters[0] = st.node_visits;
+        counters[1] = st.prim_tests;
+    }
+    return r;
+}
+
+pt_status pt_debug_trace_frame_ex(pt_scene* s, int n, const float* rays7, int any, int32_t* out_prim,
+                                  pt_stats* stats) {
     return guarded([&] {
         if (!s || n < 0 || (n && (!rays7 || !out_prim))) throw PtError(PT_ERR_INVALID_ARG, "null argument");
-        if (counters) counters[0] = counters[1] = 0;
+        if (stats) *stats = pt_stats{};
         if (n == 0) return;
         HIPCHK(hipSetDevice(s->device));
         Work w;
@@ -2207,6 +2377,7 @@ pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, 
         HIPCHK(hipMemcpy(any ? w.rayA.p : w.ray.p, soa.data(), soa.size() * sizeof(float), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(w.rq0.p, rq.data(), rq.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(w.stats.p, 0, sizeof(DevStats)));
+        HIPCHK(hipMemset(w.stats_rt.p, 0, sizeof(DevStats)));
         hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(1), 0, 0, w.counts.p, (uint32_t)n, 0u);
         launch_trace(s, w, ps, w.rq0.p, w.counts.p, (uint32_t)n, 0);
         HIPCHK(hipGetLastError());
@@ -2214,11 +2385,12 @@ pt_status pt_debug_trace_frame(pt_scene* s, int n, const float* rays7, int any, 
         // the head's hit words (device.h): hit for closest-hit queries, hitA for any-hit ones
         HIPCHK(hipMemcpy(out_prim, (const int*)w.head.p + (size_t)(any ? kHdHitA : kHdHit) * n, sizeof(int32_t) * n,
                          hipMemcpyDeviceToHost));
-        if (counters) {
-            DevStats d;
-            HIPCHK(hipMemcpy(&d, w.stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
-            counters[0] = d.nodes;
-            counters[1] = d.prims;
+        if (stats) {
+            const DevStats d = read_stats(w);
+            RenderResult rr;
+            rr.st = d;
+            rr.wide = s->wide_lds_bytes && !s->count_bytes;
+            fill_stats(rr, stats);
         }
     });
 }

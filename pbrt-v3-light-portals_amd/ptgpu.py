@@ -39,7 +39,9 @@ class pt_stats(ctypes.Structure):
                 ("render_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
                 ("trace_launches", ctypes.c_uint64), ("shade_ms", ctypes.c_double),
                 ("shade_launches", ctypes.c_uint64), ("shade_bytes", ctypes.c_uint64),
-                ("reduce_ms", ctypes.c_double)]
+                ("reduce_ms", ctypes.c_double), ("retraced_rays", ctypes.c_uint64),
+                ("wide_node_visits", ctypes.c_uint64), ("wide_prim_tests", ctypes.c_uint64),
+                ("trace_wide", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -103,6 +105,7 @@ def lib() -> ctypes.CDLL:
     L.pt_debug_camera_rays.argtypes = [vp, ctypes.c_int, vp, vp]
     L.pt_debug_trace.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
     L.pt_debug_trace_frame.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
+    L.pt_debug_trace_frame_ex.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, ctypes.POINTER(pt_stats)]
     L.pt_debug_bsdf.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
     _lib = L
     return L
@@ -321,7 +324,7 @@ class Scene:
 
     QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4,
                   "trace_kernel": 5, "shade_kernel": 6}
-    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds", 5: "k_trace_oct"}
+    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds", 5: "k_trace_oct", 6: "k_trace_w"}
     SHADE_KERNELS = {0: "k_shade", 3: "k_shade_w3", 4: "k_shade_w3h", 5: "k_shade_tab", 6: "k_shade_dl", 7: "k_shade_hero",
                      8: "k_shade_hero_w2", 9: "k_shade_hero_w4"}
 
@@ -432,6 +435,15 @@ class Scene:
         _check(lib().pt_debug_trace_frame(self._s, len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data,
                                           cnt.ctypes.data))
         return out, int(cnt[0]), int(cnt[1])
+
+    def debug_trace_frame_stats(self, rays7: np.ndarray, any_hit: bool) -> Tuple[np.ndarray, dict]:
+        """The queries through the frame's traversal kernel: (hits, the traversal's pt_stats)."""
+        rays7 = np.ascontiguousarray(rays7, np.float32)
+        out = np.zeros(len(rays7), np.int32)
+        st = pt_stats()
+        _check(lib().pt_debug_trace_frame_ex(self._s, len(rays7), rays7.ctypes.data, int(any_hit), out.ctypes.data,
+                                             ctypes.byref(st)))
+        return out, st.as_dict()
 
     def debug_bsdf(self, material: int, rec8: np.ndarray) -> np.ndarray:
         """(n, 8) records wo, wi, u0, u1 -> (n, 8) f, pdf, sampled wi, sampled pdf."""

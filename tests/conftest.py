@@ -106,3 +106,23 @@ WorldEnd
     with open(p, "w") as f:
         f.write(txt)
     return p
+
+
+# The reference's node-visit / primitive-test counters depend on its visit order.  The 4-wide traversal
+# (k_trace_w, the default for LDS-resident scenes without spheres) returns the reference's hits in another
+# order: its renders report trace_wide = 1, and node_visits / prim_tests then count only the rays it handed
+# back to the binary traversal.  Renders with set_count_bytes(True) traverse in the reference's order
+# throughout and report the reference's counters (test_gpu_parity.py::test_counting_frame_*).
+ORDER_COUNTERS = ("node_visits", "prim_tests")
+
+
+def assert_counters(gst, rst, keys):
+    """GPU render counters against the oracle's: rays and samples always, the
+    order-dependent node / primitive counters when the render traversed in the
+    reference's order."""
+    for k in keys:
+        if k in ORDER_COUNTERS and gst.get("trace_wide"):
+            continue
+        assert gst[k] == rst[k], (k, gst[k], rst[k])
+    if gst.get("trace_wide"):
+        assert gst["retraced_rays"] <= gst["closest_rays"] + gst["shadow_rays"]

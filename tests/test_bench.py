@@ -40,7 +40,9 @@ def test_kernel_match_is_exact():
 
 def _timed(trace_ms, shade_ms):
     return {"trace_ms": trace_ms, "trace_launches": 100, "shade_ms": shade_ms, "shade_launches": 100,
-            "node_visits": 10 ** 9, "prim_tests": 10 ** 8, "shade_bytes": 10 ** 12}
+            "node_visits": 10 ** 9, "prim_tests": 10 ** 8, "shade_bytes": 10 ** 12,
+            # the counting frame's reference counters (the binary traversal's visit order)
+            "node_visits_ref": 10 ** 9, "prim_tests_ref": 10 ** 8, "trace_launches_counted": 100}
 
 
 def test_roofline_kernel_is_isolated_dominant_and_traffic_needs_same_sources(tmp_path, monkeypatch):
@@ -94,8 +96,22 @@ def test_roofline_bound_check():
     timed, iso = _timed(400.0, 500.0), _timed(350.0, 270.0)
     ok = bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_lds", "k_shade_w3"), "x", ms_per_step=340.0)
     assert ok["roofline"]["within_step"]  # 350 <= 1.05 * 340
-    with pytest.raises(bench.RooflineBoundError):
-        bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_lds", "k_shade_w3"), "x", ms_per_step=300.0)
+    # beyond the step: reported on the line (within_step false + warning), the measurement is not thrown away
+    bad = bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_lds", "k_shade_w3"), "x", ms_per_step=300.0)
+    assert not bad["roofline"]["within_step"] and "per frame > step" in bad["roofline"]["warning"]
+
+
+def test_roofline_wide_traversal_view():
+    """With the 4-wide traversal the algorithmic bytes stay the reference's
+    (counting frame: 32 B per binary node visit + 48 B per primitive test)
+    and the wide kernel's own LDS reads are reported beside them."""
+    timed, iso = _timed(400.0, 500.0), _timed(350.0, 270.0)
+    iso.update(wide_node_visits=3 * 10 ** 8, wide_prim_tests=10 ** 8, retraced_rays=10 ** 5, rays=10 ** 8)
+    out = bench.rooflines(timed, iso, "w", "c2", True, ("k_trace_w", "k_shade_w3"), "x", ms_per_step=600.0)
+    k = out["roofline_kernels"]["k_trace"]
+    assert k["algorithmic_bytes_per_launch"] == round((32.0 * 10 ** 9 + 48.0 * 10 ** 8) / 100, 1)
+    assert k["wide_view"]["bytes_per_launch"] == round((112.0 * 3 * 10 ** 8 + 48.0 * 10 ** 8) / 100, 1)
+    assert k["wide_view"]["retraced_share"] == 0.001
 
 
 @pytest.mark.gpu

@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ptgpu.lib().pt_abi_version() == 10
+    assert ptgpu.lib().pt_abi_version() == 11
 
 
 def test_pt_h_compiles_as_c():

@@ -11,7 +11,7 @@ import pytest
 
 import ptgpu
 import pyoracle
-from conftest import furnace_scene
+from conftest import assert_counters, furnace_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -120,7 +120,8 @@ def _edge_rays(sc, n_rand, n_edge, seed, tmax):
 
 
 TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders with
-    "k_trace_lds": {},
+    "k_trace_w": {},
+    "k_trace_lds": {"PT_TRACE_WIDE": "0"},
     "k_trace_oct": {"PT_TRACE_OCT": "1"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
     "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
@@ -141,15 +142,18 @@ def test_frame_traversal_kernels_bit_exact(variant, monkeypatch, kernel, any_hit
     hs, sc = _scene(variant(**MINI))
     rays = _edge_rays(sc, 6000, 6000, 5, np.inf if not any_hit else 300.0)
     _, order = sc.bvh()
+    assert sc.kernel_names()[0] == {"k_trace_nb_lds": "k_trace_nb", "k_trace_nb_hbm": "k_trace_nb",
+                                    "k_trace_pt_spill": "k_trace_pt"}.get(kernel, kernel)
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
     if not any_hit:
         got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
     assert np.array_equal(got, ref)
-    assert (nodes, prims) == (rnodes, rprims)
+    if kernel != "k_trace_w":  # k_trace_w's node / prim counters cover only the rays it retraced
+        assert (nodes, prims) == (rnodes, rprims)
 
 
-@pytest.mark.parametrize("kernel", ["k_trace_lds", "k_trace_pt", "k_trace_nb_hbm"])
+@pytest.mark.parametrize("kernel", ["k_trace_w", "k_trace_lds", "k_trace_pt", "k_trace_nb_hbm"])
 def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel):
     """The box test's tMax comparison (tMin < ray.tMax) at the edge values:
     0, +-denormals, the denormal range, NaN, negative and random finite tMax
@@ -173,7 +177,8 @@ def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel):
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
     assert np.array_equal(got, ref)
-    assert (nodes, prims) == (rnodes, rprims)
+    if kernel != "k_trace_w":
+        assert (nodes, prims) == (rnodes, rprims)
 
 
 def test_bvh_device_matches_oracle(variant):
@@ -204,8 +209,7 @@ def test_render_matches_oracle(variant, strategy):
           f"rays gpu={gst['closest_rays']}/{gst['shadow_rays']} oracle={rst['closest_rays']}/{rst['shadow_rays']}")
     assert rmse / scale < 1e-4          # north_star tolerance
     assert exact == 1.0                 # in fact bit-identical (same float ops, same order)
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_render_accum_tiles_partition(variant):
@@ -268,7 +272,8 @@ def test_tile_groups_batching_equal(variant):
 
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
-                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_OCT": "1"}])
+                                 {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_OCT": "1"},
+                                 {"PT_TRACE_WIDE": "0"}, {"PT_LEAF_MIN_W": "1"}, {"PT_LEAF_MIN_W": "64"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the
@@ -279,7 +284,7 @@ def test_trace_variants_bit_exact(variant, monkeypatch, env):
     got, gst = sc.render()
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    assert gst["node_visits"] == rst["node_visits"]
+    assert_counters(gst, rst, ("closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 SHADE_VARIANTS = [
@@ -316,8 +321,7 @@ def test_shade_variants_bit_exact(tmp_path, monkeypatch, scene, env):
     got, gst = sc.render()
     ref, rst = pyoracle.render(hs.desc, nthreads=8)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_shade_variant_rejects_unknown(variant, monkeypatch):
@@ -596,8 +600,7 @@ def test_portal_room_matches_oracle(tmp_path, strategy):
     print(f"room/{strategy}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_cornell_dielectric_matches_oracle(tmp_path):
@@ -613,8 +616,7 @@ def test_cornell_dielectric_matches_oracle(tmp_path):
     assert ref.mean() > 0
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 @pytest.mark.parametrize("integrator", ["mypath", "directlighting"])
@@ -633,8 +635,7 @@ def test_killeroo_simple_matches_oracle(tmp_path, integrator):
     print(f"killeroo/{integrator}: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
     assert ref.mean() > 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_killeroo_atrium_matches_oracle(tmp_path):
@@ -661,8 +662,7 @@ def test_killeroo_atrium_matches_oracle(tmp_path):
     print(f"atrium12: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g}")
     assert ref.mean() > 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_killeroo_atrium_full_scale_matches_oracle(tmp_path):
@@ -679,8 +679,7 @@ def test_killeroo_atrium_full_scale_matches_oracle(tmp_path):
     print(f"atrium300: mean={ref.mean():.5g} rmse={_rmse(got, ref):.3g} nodes={gst['node_visits']}")
     assert ref.mean() > 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 LAMP_AS_PATH = [('Integrator "directlighting"', 'Integrator "path" "integer maxdepth" [5]'),
@@ -708,8 +707,7 @@ def test_lamp_matches_oracle(tmp_path, integrator, strategy):
     assert ref.mean() > 0
     assert _rmse(got, ref) / max(1.0, float(ref.mean())) < 1e-4
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 @pytest.mark.parametrize("filt,spp", [("gaussian", 70), ("box", 9), ("gaussian3", 5)])
@@ -807,8 +805,7 @@ def test_full_config_sparse_tiles_bit_exact():
     ref, rst = pyoracle.render_accum(hs.desc, nthreads=16, tile_offset=0, tile_stride=400)
     assert gst["samples"] == rst["samples"] == 21 * 256 * 256
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-    for k in ("closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-        assert gst[k] == rst[k], k
+    assert_counters(gst, rst, ("closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 @pytest.mark.parametrize("equal", ["1", "2"])
@@ -831,8 +828,7 @@ def test_batch_equal_two_pipelines_bit_exact(tmp_path, monkeypatch, equal):
         got, gst = sc.render_accum(r, 3)
         ref, rst = pyoracle.render_accum(hs.desc, nthreads=8, tile_offset=r, tile_stride=3)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-        for k in ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-            assert gst[k] == rst[k], k
+        assert_counters(gst, rst, ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_default_pipelines_follow_bvh_residency(tmp_path, monkeypatch):
@@ -850,8 +846,7 @@ def test_default_pipelines_follow_bvh_residency(tmp_path, monkeypatch):
         assert sc.query("pipelines") == pipes
         got, gst = sc.render_accum(0, 1)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
-        for k in ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"):
-            assert gst[k] == rst[k], k
+        assert_counters(gst, rst, ("samples", "closest_rays", "shadow_rays", "node_visits", "prim_tests"))
 
 
 def test_count_bytes_build_renders_the_same(variant):

@@ -42,7 +42,7 @@ import pytest
 
 import ptgpu
 import pyoracle
-from conftest import SCENES, scene_variant
+from conftest import SCENES, assert_counters, scene_variant
 
 COUNTERS = ("camera_rays", "closest_rays", "shadow_rays", "node_visits", "prim_tests")
 AS_PATH = [('Integrator "directlighting"', 'Integrator "path"'), ('"integer maxdepth" [10]', '"integer maxdepth" [5]')]
@@ -64,8 +64,7 @@ def _gpu_vs_oracle(path, nthreads=16):
           f"{gst['shadow_rays']} nodes={gst['node_visits']}")
     assert np.isfinite(ref).all()
     assert np.array_equal(_bits(got), _bits(ref)), f"rmse {rmse}"
-    for k in COUNTERS:
-        assert gst[k] == rst[k], (k, gst[k], rst[k])
+    assert_counters(gst, rst, COUNTERS)
     return ref, rst
 
 
