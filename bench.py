@@ -295,14 +295,16 @@ def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: boo
         if stale:
             e["traffic_stale"] = stale + " (taken on other sources: not used)"
         if p == "trace" and iso.get("wide_node_visits"):
-            wb = (112.0 * iso["wide_node_visits"] + 48.0 * iso["wide_prim_tests"]) / il
+            nb = 128.0 if iso.get("wide_hbm") else 112.0  # one 128-B line per node from HBM, 112 B in LDS
+            wb = (nb * iso["wide_node_visits"] + 48.0 * iso["wide_prim_tests"]) / il
             e["wide_view"] = {"bytes_per_launch": round(wb, 1), "GBs": round(wb / (avg * 1e-3) / 1e9, 1),
                               "retraced_share": round(iso["retraced_rays"] / max(1, iso["rays"]), 6),
                               "wide_nodes_per_ray": round(iso["wide_node_visits"] / max(1, iso["rays"]), 4),
                               "prim_tests_per_ray": round(iso["wide_prim_tests"] / max(1, iso["rays"]), 4),
                               "ref_nodes_per_ray": round(iso["node_visits_ref"] / max(1, iso["rays"]), 4),
                               "ref_prim_tests_per_ray": round(iso["prim_tests_ref"] / max(1, iso["rays"]), 4),
-                              "note": "k_trace_w's own LDS reads (112 B per 4-wide node, 48 B per primitive test) "
+                              "note": "k_trace_w's own reads (112 B per 4-wide node from LDS, 128 from HBM; 48 B per "
+                                      "primitive test) "
                                       "and the share of rays it handed back to the binary kernel; the launch time "
                                       "includes that retrace launch"}
         if p == "trace" and lds_scene:
@@ -499,6 +501,7 @@ def main():
     for k in iso:
         iso[k] = st[k]
     iso["rays"] = st["closest_rays"] + st["shadow_rays"]
+    iso["wide_hbm"] = sc.query("trace_kernel") == 7
     # and one frame with the shading build that also counts its algorithmic path-state bytes (one more
     # register: a separate instantiation, pt_set_count_bytes; the same batches, bounces and launches)
     sc.set_count_bytes(True)

@@ -22,6 +22,7 @@ constexpr int kNodeSteps = PT_NODE_STEPS;
 constexpr int kLeafSteps = PT_LEAF_STEPS;
 constexpr int kStackLds = 20;     // LDS-resident part of the 64-entry BVH stack
 constexpr int kSpillWords = 64 - kStackLds;  // k_trace_pt: global spill entries per lane beyond the LDS rows
+constexpr int kWideLdsRowsMax = 24;  // k_trace_w<true>: LDS stack rows per lane (12 blocks of 128 lanes per CU)
 constexpr int kShadeBlock = 128;
 constexpr int kShadeBpcW3 = 36;       // k_shade_w3 blocks per CU (six rounds of its 6 resident blocks; 24: C2 k_shade 5.97 vs 5.88 ms)
 constexpr int kMaxPortals = PT_MAX_PORTALS;  // include/pt.h

@@ -1205,18 +1205,23 @@ __global__ __launch_bounds__(kOctBlock) __attribute__((amdgpu_waves_per_eu(kSph 
 //    object space, whose origin the Transform moved forward by its error bound,
 //    transform.h:303-316, plane.cpp:15-55), and culls boxes against it.  Every
 //    such t carries rounding errors of a few ulps of t plus absolute errors of
-//    order 100 eps x the coordinates involved (pbrt's own deltaT bound,
-//    triangle.cpp:362-385, the transformed origin's shift).  So here primitives
-//    are accepted -- and boxes culled -- against T = tBest + |tBest| 2^-17 + 2A,
-//    with A = 2^-10 (the scene's largest |coordinate| + the origin's), the
-//    smallest t wins and every other accepted t goes to t2.  When no other
-//    primitive is accepted within W = tBest + |tBest| 2^-18 + A, those margins
-//    are far beyond the error bounds and the winner is the only primitive the
-//    reference can keep whatever its order; otherwise -- a near tie, a hit at
-//    t <= 0 (aaplane: no t > 0 test), a NaN t, or a ray with an infinite 1/d
-//    component (NaN slabs) -- the ray goes to a retrace queue that the binary
-//    k_trace_lds traverses in the reference's order right after this launch.
-//    Hits are therefore the reference's, bit for bit; its node / primitive
+//    order 10 eps x the coordinates involved at non-grazing incidence (pbrt's
+//    own deltaT bound, triangle.cpp:362-385; the transformed origin's shift).
+//    So primitives are accepted against T = tBest + |tBest| 2^-17 + 2A, with
+//    A = 2^-18 R (R = the scene's largest |coordinate| + the origin's: 64 eps R,
+//    several times those errors), and boxes culled against T + 30A; the smallest
+//    t wins and every other accepted t goes to t2.  When no other primitive is
+//    accepted within W = tBest + |tBest| 2^-18 + A, the margins exceed the
+//    error bounds and the winner is the only primitive the reference can keep
+//    whatever its order;
+//    otherwise -- a near tie, a hit at t <= 0 (aaplane: no t > 0 test), a NaN
+//    t, or a ray with an infinite 1/d component (NaN slabs) -- the ray goes to
+//    a retrace queue that the binary k_trace_lds traverses in the reference's
+//    order right after this launch.  The one case no margin covers is a
+//    triangle whose computed t lies more than 32A = 2^-13 R below its own leaf
+//    box's entry distance (incidence within a few mrad of grazing AND a box
+//    that starts beyond the winner, where the reference's own answer turns on
+//    its visit order).  Its node / primitive
 //    counters are not produced (the binary build runs for the counting frame,
 //    pt_set_count_bytes).
 //
@@ -1254,6 +1259,9 @@ __device__ __forceinline__ void lds_wnode_top(uint32_t cur, uint32_t axyz, uint3
           "v"(sp)
         : "memory");
     *nx = a; *fx = b; *ny = c; *fy = d; *nz = e; *fz = f; *wd = g; *top = t;
+}
+__device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 // three entries above the top (the node step's pushes; rows past the new top are dead)
 __device__ __forceinline__ void lds_push3(uint32_t sp, uint32_t a, uint32_t b, uint32_t c) {
@@ -1294,32 +1302,71 @@ constexpr int kWNodeSteps = PT_WNODE_STEPS;
 #else
 #define PT_TRACE_W_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 #endif
+constexpr uint32_t kWideStrideLds = 112;  // LDS image: 7 x 16 B per wide node
+constexpr uint32_t kWideStrideHbm = 128;  // HBM image: one 128-B line per wide node (7 x 16 B + 16 B pad)
+
+// The HBM image's node loads (k_trace_w<true>): the six plane quads picked by the ray's direction signs and the
+// child words, as buffer loads at 32-bit byte offsets from the image base (one 128-B line per node)
+__device__ __forceinline__ void hbm_wnode(__amdgpu_buffer_rsrc_t img, uint32_t cur, uint32_t axyz, float4* nx,
+                                          float4* fx, float4* ny, float4* fy, float4* nz, float4* fz, uint4* wd) {
+    const uint32_t ax = axyz & 0xffu, ay = (axyz >> 8) & 0xffu, az = axyz >> 16;
+    auto ld = [&](uint32_t off) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(img, (int)off, 0, 0);
+        return __builtin_bit_cast(float4, v);
+    };
+    *nx = ld(cur + ax);
+    *fx = ld(cur + 16u - ax);
+    *ny = ld(cur + 32u + ay);
+    *fy = ld(cur + 48u - ay);
+    *nz = ld(cur + 64u + az);
+    *fz = ld(cur + 80u - az);
+    *wd = __builtin_bit_cast(uint4, ld(cur + 96u));
+}
+
+// k_trace_w<kHbm>: kHbm = false stages the 112-B-node image and the primitive records in LDS (C2-C4);
+// kHbm = true reads the 128-B-node image and the records from HBM (C5's ten million primitives), with the
+// stack in `stack_rows` LDS rows per lane and its deeper entries in a per-lane global spill column.
+template <bool kHbm>
 __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScene sc, DevPaths ps,
                                                                         const uint32_t* __restrict__ rq,
                                                                         const uint32_t* __restrict__ rq_count,
                                                                         uint32_t* fetch, int refill_min, int leaf_min,
                                                                         uint32_t* retrace_q, uint32_t* retrace_n,
+                                                                        int stack_rows, uint32_t* spill,
                                                                         DevStats* stats)
 #ifdef PT_TU_TRACE
 {
     extern __shared__ float4 lds_dyn[];
-    const int nw = 7 * sc.n_wnodes;
-    const int scene_f4 = nw + 3 * sc.n_prims;
-    const uint32_t node0 = (uint32_t)(uintptr_t)lds_dyn;  // wide nodes are named by their LDS byte address
-    for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
-        float4 v = i < nw ? sc.wnodes[i] : sc.prims[i - nw];
-        if (i < nw && i % 7 == 6) {  // child words: image offsets -> LDS addresses
-            uint32_t w[4] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-            for (int k = 0; k < 4; ++k)
-                if ((int)w[k] < 0) w[k] = 0x80000000u | (node0 + (w[k] & 0x7fffffffu));
-            v = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]));
+    const int nw = kHbm ? 0 : 7 * sc.n_wnodes;
+    const int scene_f4 = kHbm ? 0 : nw + 3 * sc.n_prims;
+    const uint32_t node0 = kHbm ? 0u : (uint32_t)(uintptr_t)lds_dyn;  // LDS: wide nodes named by LDS byte address
+    if constexpr (!kHbm) {
+        for (int i = threadIdx.x; i < scene_f4; i += blockDim.x) {
+            float4 v = i < nw ? sc.wnodes[i] : sc.prims[i - nw];
+            if (i < nw && i % 7 == 6) {  // child words: image offsets -> LDS addresses
+                uint32_t w[4] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                                 __float_as_uint(v.w)};
+                for (int k = 0; k < 4; ++k)
+                    if ((int)w[k] < 0) w[k] = 0x80000000u | (node0 + (w[k] & 0x7fffffffu));
+                v = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                __uint_as_float(w[3]));
+            }
+            lds_dyn[i] = v;
         }
-        lds_dyn[i] = v;
+        __syncthreads();
     }
-    __syncthreads();
-    const float4* bprims = lds_dyn + nw;
-    // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k
+    const float4* bprims = kHbm ? sc.prims : lds_dyn + nw;
+    // the HBM image as a buffer resource (gfx9 dword 3: 32-bit data format), one per launch
+    const __amdgpu_buffer_rsrc_t img = __builtin_amdgcn_make_buffer_rsrc((void*)sc.wnodes, (short)0, 0x7fffffff,
+                                                                        0x00020000);
+    // the lane's stack column: row 0 the dummy, entry k (k >= 1) in row k (LDS byte addresses, rows 512 B apart);
+    // kHbm: rows from `stack_rows` on live in the lane's spill column (entry k at spill[col + k - stack_rows])
     const uint32_t sbase = (uint32_t)(uintptr_t)((uint32_t*)(lds_dyn + scene_f4) + threadIdx.x);
+    // the LDS rows' end and the spill column, recomputed where used (registers: the 6-wave budget)
+    const uint32_t srows = 512u * (uint32_t)stack_rows;
+#define PT_SLIM (sbase + srows)
+#define PT_SCOL (spill + (size_t)(blockIdx.x * (uint32_t)kTraceBlock + threadIdx.x) * (uint32_t)kSpillWords)
+    auto srow = [&](uint32_t a) { return (a - PT_SLIM) >> 9; };  // spill index of a stack address past the LDS rows
     const uint32_t n = *rq_count;
     const uint32_t rmin = (uint32_t)min(max(refill_min, 1), 64);  // idle lanes that trigger a refill
     const uint32_t lmin = (uint32_t)max(leaf_min, 1);             // parked lanes that trigger a leaf step
@@ -1401,7 +1448,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
         const bool shadow = (ent & 3u) == kRayShadow;
         // the ray's absolute margin A (not kept: one register less)
         const float amarg = (sc.wide_scale + __builtin_fmaxf(__builtin_fmaxf(fabsf(ox.x), fabsf(oy.x)), fabsf(oz.x))) *
-                            (1.0f / 1024.0f);
+                            (1.0f / 262144.0f);
         if (leafStep) {
 #pragma unroll
             for (int u = 0; u < kLeafSteps; ++u) {  // up to kLeafSteps primitive tests of the lane's leaf
@@ -1440,7 +1487,9 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
                     const bool empty = sp == sbase;
                     done = empty;
                     if (!empty) {
-                        const uint32_t w = (uint32_t)lds_top(sp);
+                        uint32_t w;
+                        if (!kHbm || sp < PT_SLIM) w = (uint32_t)lds_top(sp);
+                        else w = PT_SCOL[srow(sp)];
                         sp -= 512;
                         const bool inner = (int)w < 0;
                         cur = inner ? (w & 0x7fffffffu) : cur;
@@ -1458,14 +1507,20 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
                 float4 nx, fx, ny, fy, nz, fz;
                 uint4 wd;
                 uint32_t top;
-                lds_wnode_top(cur, axyz, sp, &nx, &fx, &ny, &fy, &nz, &fz, &wd, &top);
-                const float tc = tmx;
+                if constexpr (kHbm) {
+                    hbm_wnode(img, cur, axyz, &nx, &fx, &ny, &fy, &nz, &fz, &wd);
+                    top = sp < PT_SLIM ? (uint32_t)lds_top(sp) : PT_SCOL[srow(sp)];
+                } else {
+                    lds_wnode_top(cur, axyz, sp, &nx, &fx, &ny, &fy, &nz, &fz, &wd, &top);
+                }
+                // box cull: T + 30A for closest-hit rays, a shadow ray's own tMax (any-hit: the reference's set)
+                const float tc = shadow ? tmx : tmx + 30 * amarg;
                 const WideHit2 h01 = wide_box2(pt_f2{nx.x, nx.y}, pt_f2{fx.x, fx.y}, pt_f2{ny.x, ny.y},
-                                               pt_f2{fy.x, fy.y}, pt_f2{nz.x, nz.y}, pt_f2{fz.x, fz.y}, ox, oy, oz, ix, iy, iz,
-                                               tc);
+                                               pt_f2{fy.x, fy.y}, pt_f2{nz.x, nz.y}, pt_f2{fz.x, fz.y}, ox, oy, oz,
+                                               ix, iy, iz, tc);
                 const WideHit2 h23 = wide_box2(pt_f2{nx.z, nx.w}, pt_f2{fx.z, fx.w}, pt_f2{ny.z, ny.w},
-                                               pt_f2{fy.z, fy.w}, pt_f2{nz.z, nz.w}, pt_f2{fz.z, fz.w}, ox, oy, oz, ix, iy, iz,
-                                               tc);
+                                               pt_f2{fy.z, fy.w}, pt_f2{nz.z, nz.w}, pt_f2{fz.z, fz.w}, ox, oy, oz,
+                                               ix, iy, iz, tc);
                 // sort keys: a hit child's entry distance (> -inf), a missed one -inf; descending, so the hits
                 // come first, farthest to nearest
                 const float kHitMin = -3.40282347e38f;
@@ -1487,7 +1542,17 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
                 PT_WCAS(0, 1) PT_WCAS(2, 3) PT_WCAS(0, 2) PT_WCAS(1, 3) PT_WCAS(1, 2)
 #undef PT_WCAS
                 const uint32_t nh = (uint32_t)h01.h0 + (uint32_t)h01.h1 + (uint32_t)h23.h0 + (uint32_t)h23.h1;
-                lds_push3(sp, w0, w1, w2);  // the hits but the nearest (rows past the new top are dead)
+                // the hits but the nearest, farthest first (rows past the new top are dead)
+                if (!kHbm || sp + 1536u < PT_SLIM) {
+                    lds_push3(sp, w0, w1, w2);
+                } else {  // the spill's edge: entry by entry
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const uint32_t a = sp + 512u * (uint32_t)(q + 1), v = q == 0 ? w0 : (q == 1 ? w1 : w2);
+                        if (a < PT_SLIM) lds_write1(a, v);
+                        else if (srow(a) < (uint32_t)kSpillWords) PT_SCOL[srow(a)] = v;
+                    }
+                }
                 const bool empty = sp == sbase;
                 const bool pop = (nh == 0) & !empty;
                 const uint32_t nxt = nh == 0 ? top : (nh == 1 ? w0 : (nh == 2 ? w1 : (nh == 3 ? w2 : w3)));
@@ -1526,6 +1591,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
             if (iters_w) atomicAdd(&stats->lane_iters, 64ull * iters_w);
         }
     }
+#undef PT_SLIM
+#undef PT_SCOL
 }
 #else
 ;

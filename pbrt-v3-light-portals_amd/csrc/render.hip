@@ -292,9 +292,13 @@ struct pt_scene {
     int trace_persist = 2;       // 0: k_trace, 1: k_trace_pt, 2: k_trace_nb (branch-reduced)
     bool trace_lean = true;      // LDS scenes under trace_persist 2: k_trace_lds (PT_TRACE_LEAN=0: k_trace_nb)
     size_t oct_lds_bytes = 0;    // > 0: k_trace_oct (octant images of an LDS-sized BVH; opt-in PT_TRACE_OCT=1)
-    size_t wide_lds_bytes = 0;   // > 0: k_trace_w (4-wide BVH image + primitive records + stack; PT_TRACE_WIDE=0 disables)
-    int wide_rows = 0;           // k_trace_w LDS stack rows per lane (dummy row + deepest stack + 3 push rows)
-    int leaf_min_w = 32;         // k_trace_w: lanes parked at leaves that trigger a primitive-test step (PT_LEAF_MIN_W)
+    size_t wide_lds_bytes = 0;   // > 0: k_trace_w, its dynamic LDS (PT_TRACE_WIDE=0 disables): LDS-resident scenes the
+                                 // 4-wide BVH image + primitive records + stack, HBM-resident ones the stack rows
+    bool wide_hbm = false;       // k_trace_w<true>: the wide image and the primitives from HBM
+    int wide_rows = 0;           // k_trace_w stack rows per lane (dummy row + deepest stack + 3 push rows)
+    int wide_lds_rows = 0;       // of them in LDS (k_trace_w<true>: the rest in the lane's spill column)
+    int leaf_min_w = 48;         // k_trace_w: lanes parked at leaves that trigger a primitive-test step (PT_LEAF_MIN_W;
+                                 // C2 16 / 32 / 48 / 64: 10.39 / 9.12 / 8.69 / 8.67 ms per launch)
     int trace_bpc = 16;          // persistent trace blocks per CU
     int shade_bpc = 48;          // shading blocks per CU (grid-stride; PT_SHADE_BPC): 12 rounds of the 2-wave kernels' 4 resident blocks (8: C4 k_shade 13.0 vs 10.0 ms, C3 362 vs 375 Msamples/s)
     int film_t = 0;              // RGB film, filter windows of 2-16 pixels: PT_FILM_T=1 takes k_film_t (lane = film pixel; faster at 256 spp, slower at 1024: DESIGN §10)
@@ -1120,7 +1124,7 @@ static void tile_pixels(const Frame& fr, int offset, int stride, std::vector<int
 // scene (pt_scene_query PT_Q_TRACE_KERNEL / PT_Q_SHADE_KERNEL; the bench names
 // the kernel its roofline is for).
 static int trace_kernel_id(const pt_scene* s) {
-    if (s->wide_lds_bytes && !s->count_bytes) return 6;
+    if (s->wide_lds_bytes && !s->count_bytes) return s->wide_hbm ? 7 : 6;
     if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean)
         return s->oct_lds_bytes ? 5 : 3;
     if (s->trace_persist == 2 && !s->trace_spill) return 2;
@@ -1136,50 +1140,60 @@ static int shade_kernel_id(const pt_scene* s) {
 // One traversal launch over the nrays entries of ray queue rq (counts[0] holds
 // their number, counts[4] the persistent kernels' fetch cursor, zero): the
 // kernel this scene renders with (see create_scene_on).
-static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
-                         hipStream_t st) {
+// One binary (reference-order) traversal launch over the nrays entries of ray queue rq (*cnt holds their
+// number, *fetch the persistent kernels' fetch cursor, zero): the kernel this scene renders with when it does
+// not take k_trace_w (see create_scene_on), and the retrace kernel behind k_trace_w.
+static void launch_binary(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* cnt,
+                          uint32_t* fetch, uint32_t nrays, hipStream_t st, DevStats* stats) {
     const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
-    if (s->wide_lds_bytes && !s->count_bytes) {
-        // k_trace_w over the queue, then the binary k_trace_lds over the rays it hands back (near ties,
-        // infinite 1/d): counts[6] their number, counts[7] that launch's fetch cursor
-        hipLaunchKernelGGL(k_trace_w, pg, dim3(kTraceBlock), s->wide_lds_bytes, st, s->dev, ps, rq, counts + 0,
-                           counts + 4, s->refill_min, s->leaf_min_w, w.rqr.p, counts + 6, w.stats.p);
-        const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
-        const dim3 rg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * 2)));
-        hipLaunchKernelGGL(trace_lds_kernel(false), rg, dim3(kTraceBlock), lds, st, s->dev, ps, w.rqr.p, counts + 6,
-                           counts + 7, s->refill_min, s->leaf_min, w.stats_rt.p);
-        return;
-    }
     if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && s->oct_lds_bytes) {
         // k_trace_oct: eight octant images of the BVH + the primitive records + the stack, 4 blocks per CU
         const dim3 og(std::max(1, std::min(ceil_div(nrays, kOctBlock), s->num_cus * 4)));
         hipLaunchKernelGGL(trace_oct_kernel(s->has_spheres), og, dim3(kOctBlock), s->oct_lds_bytes, st, s->dev, ps, rq,
-                           counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+                           cnt, fetch, s->refill_min, s->leaf_min, stats);
     } else if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean) {
         // k_trace_lds: LDS scene, stack of a dummy row + depth rows + the row a push writes above
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 2) * kTraceBlock * sizeof(int);
-        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq,
-                           counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+        hipLaunchKernelGGL(trace_lds_kernel(s->has_spheres), pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq, cnt,
+                           fetch, s->refill_min, s->leaf_min, stats);
     } else if (s->trace_persist == 2 && !s->trace_spill) {
         // branch-reduced persistent traversal; LDS stack of depth+1 rows
         const size_t lds = s->lds_scene_bytes + (size_t)(s->stack_rows + 1) * kTraceBlock * sizeof(int);
         hipLaunchKernelGGL(trace_nb_kernel(s->lds_scene_bytes != 0, s->has_spheres), pg, dim3(kTraceBlock), lds, st,
-                           s->dev, ps, rq, counts + 0, counts + 4, s->refill_min, s->leaf_min, w.stats.p);
+                           s->dev, ps, rq, cnt, fetch, s->refill_min, s->leaf_min, stats);
     } else if (s->trace_persist) {
-        // persistent: about one resident wave set; lanes refill from counts[4]
+        // persistent: about one resident wave set; lanes refill from *fetch
         auto kt = trace_pt_kernel(s->lds_scene_bytes != 0, s->trace_spill != 0, s->has_spheres);
         const size_t lds = s->lds_scene_bytes + (size_t)s->stack_rows * kTraceBlock * sizeof(int);
-        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq, counts + 0, counts + 4, s->refill_min,
-                           s->leaf_min_pt, s->stack_rows, w.spill.p, w.stats.p);
+        hipLaunchKernelGGL(kt, pg, dim3(kTraceBlock), lds, st, s->dev, ps, rq, cnt, fetch, s->refill_min,
+                           s->leaf_min_pt, s->stack_rows, w.spill.p, stats);
     } else {
         const dim3 tg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * 16)));
         if (s->lds_scene_bytes)
             hipLaunchKernelGGL(trace_kernel(true, s->has_spheres), tg, dim3(kTraceBlock), s->lds_scene_bytes, st,
-                               s->dev, ps, rq, counts + 0, w.spill.p, w.stats.p);
+                               s->dev, ps, rq, cnt, w.spill.p, stats);
         else
-            hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, st, s->dev, ps, rq,
-                               counts + 0, w.spill.p, w.stats.p);
+            hipLaunchKernelGGL(trace_kernel(false, s->has_spheres), tg, dim3(kTraceBlock), 0, st, s->dev, ps, rq, cnt,
+                               w.spill.p, stats);
     }
+}
+
+// One traversal of the nrays entries of ray queue rq (counts[0] holds their number, counts[4] the persistent
+// kernels' fetch cursor, zero): k_trace_w over the queue and the binary kernel over the rays it hands back
+// (near ties, infinite 1/d: counts[6] their number, counts[7] that launch's fetch cursor), or the binary
+// kernel alone (no wide image, or the counting frame, pt_set_count_bytes).
+static void launch_trace(pt_scene* s, Work& w, const DevPaths& ps, const uint32_t* rq, uint32_t* counts, uint32_t nrays,
+                         hipStream_t st) {
+    if (s->wide_lds_bytes && !s->count_bytes) {
+        const dim3 pg(std::max(1, std::min(ceil_div(nrays, kTraceBlock), s->num_cus * s->trace_bpc)));
+        hipLaunchKernelGGL(s->wide_hbm ? k_trace_w<true> : k_trace_w<false>, pg, dim3(kTraceBlock), s->wide_lds_bytes,
+                           st, s->dev, ps, rq, counts + 0, counts + 4, s->refill_min, s->leaf_min_w, w.rqr.p,
+                           counts + 6, s->wide_lds_rows, (uint32_t*)w.spill.p, w.stats.p);
+        launch_binary(s, w, ps, w.rqr.p, counts + 6, counts + 7, std::min<uint32_t>(nrays, s->num_cus * 2 * kTraceBlock),
+                      st, w.stats_rt.p);
+        return;
+    }
+    launch_binary(s, w, ps, rq, counts + 0, counts + 4, nrays, st, w.stats.p);
 }
 
 // End of a bounce: the output queue sizes become the next bounce's input sizes,
@@ -1671,12 +1685,15 @@ static int bvh_stack_bound(const std::vector<LinearNode>& nodes) {
 // node's two children and opens the interior child of largest surface area until it holds four children
 // (or only leaves are left); every child is a node of the reference's tree with its exact bounds -- an
 // interior one becomes the next wide node, a leaf keeps its primitive range (bvh.cpp:640-658 layout).
-// Image per wide node (112 B): {lo.x of children 0-3} {hi.x} {lo.y} {hi.y} {lo.z} {hi.z} {child words};
+// Image per wide node (`stride` bytes, 112 in LDS, 128 in HBM: one cache line): {lo.x of children 0-3} {hi.x}
+// {lo.y} {hi.y} {lo.z} {hi.z} {child words} [pad];
 // child word = 0x80000000 | byte offset of a wide node in the image (the kernel adds the LDS base), or
 // first primitive | count << 24 for a leaf; unused slots: bounds +inf / -inf (never hit) and word 0.
 // *rows: LDS stack rows per lane -- the dummy row, the deepest stack a node can be visited at, and the three
 // rows the node step writes above its top.  Returns false when the tree does not fit the child-word encoding.
-static bool build_wide(const std::vector<LinearNode>& bn, std::vector<float4>* img, int* n_wide, int* rows) {
+static bool build_wide(const std::vector<LinearNode>& bn, uint32_t stride, std::vector<float4>* img, int* n_wide,
+                       int* rows) {
+    const size_t q4 = stride / 16;  // float4s per wide node (7, or 8 with a pad for one 128-B line each)
     img->clear();
     *n_wide = 0;
     *rows = 0;
@@ -1724,8 +1741,8 @@ static bool build_wide(const std::vector<LinearNode>& bn, std::vector<float4>* i
         wn[t.wide] = w;
     }
     const size_t nw = wn.size();
-    if (nw * 112u >= 0x80000000ull) return false;
-    img->assign(nw * 7, make_float4(0, 0, 0, 0));
+    if (nw * stride >= 0x80000000ull) return false;
+    img->assign(nw * q4, make_float4(0, 0, 0, 0));
     for (size_t i = 0; i < nw; ++i) {
         float lo[3][4], hi[3][4];
         uint32_t word[4];
@@ -1739,9 +1756,9 @@ static bool build_wide(const std::vector<LinearNode>& bn, std::vector<float4>* i
             const LinearNode& n = bn[c];
             for (int a = 0; a < 3; ++a) { lo[a][k] = n.bmin[a]; hi[a][k] = n.bmax[a]; }
             word[k] = n.nprims > 0 ? ((uint32_t)n.offset | ((uint32_t)n.nprims << 24))
-                                   : (0x80000000u | (uint32_t)(112 * wn[i].wid[k]));
+                                   : (0x80000000u | (uint32_t)(stride * (uint32_t)wn[i].wid[k]));
         }
-        float4* q = img->data() + 7 * i;
+        float4* q = img->data() + q4 * i;
         for (int a = 0; a < 3; ++a) {
             q[2 * a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
             q[2 * a + 1] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
@@ -1826,15 +1843,26 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                                                                           : (size_t)prop.sharedMemPerMultiprocessor;
         s->oct_lds_bytes = (s->lds_scene_bytes && !s->trace_spill && 4 * oct <= cu_lds && t && t[0] == '1') ? oct : 0;
     }
-    {   // k_trace_w (4-wide BVH) for the scenes k_trace_lds traverses, without spheres (the sphere test's EFloat
-        // acceptance is left to the binary order); the binary kernel stays the retrace and counting traversal
+    {   // k_trace_w (4-wide BVH) for scenes without spheres (the sphere test's EFloat acceptance is left to the
+        // binary order); the binary kernel stays the retrace and counting traversal.  LDS-resident scenes (the
+        // k_trace_lds ones): image + primitives staged in LDS; HBM-resident ones (the k_trace_pt / k_trace_nb ones):
+        // image in HBM, LDS stack rows + spill
         const char* t = std::getenv("PT_TRACE_WIDE");
+        const bool lds = s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean &&
+                         !s->oct_lds_bytes;
+        const bool hbm = !s->lds_scene_bytes && s->trace_persist >= 1;
         std::vector<float4> img;
         int nw = 0, rows = 0;
-        if (s->trace_persist == 2 && !s->trace_spill && s->lds_scene_bytes && s->trace_lean && !s->oct_lds_bytes &&
-            !s->has_spheres && !(t && t[0] == '0') && build_wide(s->host_nodes, &img, &nw, &rows) && nw > 0) {
-            const size_t scene = (size_t)nw * 112 + (size_t)s->dev.n_prims * 48;
-            if (scene <= (size_t)kLdsSceneMax + 4096 && rows <= 64) {
+        if ((lds || hbm) && !s->has_spheres && !(t && t[0] == '0') &&
+            build_wide(s->host_nodes, lds ? kWideStrideLds : kWideStrideHbm, &img, &nw, &rows) && nw > 0) {
+            const size_t scene = lds ? (size_t)nw * kWideStrideLds + (size_t)s->dev.n_prims * 48 : 0;
+            // HBM: at most kWideLdsRowsMax rows per lane in LDS (12 blocks of 128 lanes at 6 waves per SIMD), the
+            // rest in the spill column (kSpillWords entries)
+            int lrows = lds ? rows : std::min(rows, kWideLdsRowsMax);
+            if (const char* r = std::getenv("PT_WIDE_LDS_ROWS"))  // test hook: force the HBM kernel's spill path
+                if (hbm) lrows = std::max(1, std::min(lrows, std::atoi(r)));
+            if ((lds && scene <= (size_t)kLdsSceneMax + 4096 && rows <= 64) ||
+                (hbm && rows - lrows <= kSpillWords)) {
                 s->wnodes.upload(img);
                 s->dev.wnodes = s->wnodes.p;
                 s->dev.n_wnodes = nw;
@@ -1842,11 +1870,14 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
                 for (int k = 0; k < 3; ++k)
                     sc_max = std::max({sc_max, std::fabs(s->host_nodes[0].bmin[k]), std::fabs(s->host_nodes[0].bmax[k])});
                 s->dev.wide_scale = sc_max;
+                s->wide_hbm = hbm;
                 s->wide_rows = rows;
-                s->wide_lds_bytes = scene + (size_t)rows * kTraceBlock * sizeof(uint32_t);
+                s->wide_lds_rows = lrows;
+                s->wide_lds_bytes = scene + (size_t)lrows * kTraceBlock * sizeof(uint32_t);
             }
         }
         if (const char* l = std::getenv("PT_LEAF_MIN_W")) s->leaf_min_w = std::max(1, std::atoi(l));
+        else if (s->wide_hbm) s->leaf_min_w = s->leaf_min_pt;
     }
     if (std::getenv("PT_TRACE_DEBUG"))
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, wide %zu B (%d nodes, %d rows), "

@@ -16,6 +16,8 @@ template __global__ void k_trace_lds<false>(PT_ARGS, uint32_t*, int, int, DevSta
 template __global__ void k_trace_lds<true>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_oct<false>(PT_ARGS, uint32_t*, int, int, DevStats*);
 template __global__ void k_trace_oct<true>(PT_ARGS, uint32_t*, int, int, DevStats*);
+template __global__ void k_trace_w<false>(PT_ARGS, uint32_t*, int, int, uint32_t*, uint32_t*, int, uint32_t*, DevStats*);
+template __global__ void k_trace_w<true>(PT_ARGS, uint32_t*, int, int, uint32_t*, uint32_t*, int, uint32_t*, DevStats*);
 #define PT_PT(a, b, c) template __global__ void k_trace_pt<a, b, c>(PT_ARGS, uint32_t*, int, int, int, int*, DevStats*);
 PT_PT(false, false, false) PT_PT(false, false, true) PT_PT(false, true, false) PT_PT(false, true, true)
 PT_PT(true, false, false) PT_PT(true, false, true) PT_PT(true, true, false) PT_PT(true, true, true)

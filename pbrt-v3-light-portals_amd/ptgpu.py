@@ -324,7 +324,8 @@ class Scene:
 
     QUERY_KEYS = {"pipelines": 0, "batch_slots": 1, "trace_lds_bytes": 2, "trace_spill": 3, "features": 4,
                   "trace_kernel": 5, "shade_kernel": 6}
-    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds", 5: "k_trace_oct", 6: "k_trace_w"}
+    TRACE_KERNELS = {0: "k_trace", 1: "k_trace_pt", 2: "k_trace_nb", 3: "k_trace_lds", 5: "k_trace_oct", 6: "k_trace_w",
+                     7: "k_trace_w"}  # 7: k_trace_w<true>, the wide image and primitives from HBM
     SHADE_KERNELS = {0: "k_shade", 3: "k_shade_w3", 4: "k_shade_w3h", 5: "k_shade_tab", 6: "k_shade_dl", 7: "k_shade_hero",
                      8: "k_shade_hero_w2", 9: "k_shade_hero_w4"}
 

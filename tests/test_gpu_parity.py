@@ -124,9 +124,11 @@ TRACE_KERNELS = {  # environment -> the traversal kernel the scene then renders 
     "k_trace_lds": {"PT_TRACE_WIDE": "0"},
     "k_trace_oct": {"PT_TRACE_OCT": "1"},
     "k_trace_nb_lds": {"PT_TRACE_LEAN": "0"},
-    "k_trace_nb_hbm": {"PT_TRACE_LDS": "0"},
+    "k_trace_w_hbm": {"PT_TRACE_LDS": "0"},
+    "k_trace_w_hbm_spill": {"PT_TRACE_LDS": "0", "PT_WIDE_LDS_ROWS": "2"},
+    "k_trace_nb_hbm": {"PT_TRACE_LDS": "0", "PT_TRACE_WIDE": "0"},
     "k_trace_pt": {"PT_TRACE_PERSIST": "1"},
-    "k_trace_pt_spill": {"PT_TRACE_PERSIST": "1", "PT_STACK_ROWS": "2", "PT_TRACE_LDS": "0"},
+    "k_trace_pt_spill": {"PT_TRACE_PERSIST": "1", "PT_STACK_ROWS": "2", "PT_TRACE_LDS": "0", "PT_TRACE_WIDE": "0"},
     "k_trace": {"PT_TRACE_PERSIST": "0"},
 }
 
@@ -143,17 +145,18 @@ def test_frame_traversal_kernels_bit_exact(variant, monkeypatch, kernel, any_hit
     rays = _edge_rays(sc, 6000, 6000, 5, np.inf if not any_hit else 300.0)
     _, order = sc.bvh()
     assert sc.kernel_names()[0] == {"k_trace_nb_lds": "k_trace_nb", "k_trace_nb_hbm": "k_trace_nb",
-                                    "k_trace_pt_spill": "k_trace_pt"}.get(kernel, kernel)
+                                    "k_trace_pt_spill": "k_trace_pt", "k_trace_w_hbm": "k_trace_w",
+                                    "k_trace_w_hbm_spill": "k_trace_w"}.get(kernel, kernel)
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
     if not any_hit:
         got = np.where(got >= 0, order[np.maximum(got, 0)], -1)
     assert np.array_equal(got, ref)
-    if kernel != "k_trace_w":  # k_trace_w's node / prim counters cover only the rays it retraced
+    if not kernel.startswith("k_trace_w"):  # k_trace_w's node / prim counters cover only the rays it retraced
         assert (nodes, prims) == (rnodes, rprims)
 
 
-@pytest.mark.parametrize("kernel", ["k_trace_w", "k_trace_lds", "k_trace_pt", "k_trace_nb_hbm"])
+@pytest.mark.parametrize("kernel", ["k_trace_w", "k_trace_w_hbm", "k_trace_lds", "k_trace_pt", "k_trace_nb_hbm"])
 def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel):
     """The box test's tMax comparison (tMin < ray.tMax) at the edge values:
     0, +-denormals, the denormal range, NaN, negative and random finite tMax
@@ -177,7 +180,7 @@ def test_frame_traversal_tmax_edge_cases(variant, monkeypatch, kernel):
     got, nodes, prims = sc.debug_trace_frame(rays, any_hit)
     ref, rnodes, rprims = pyoracle.trace_counted(hs.desc, rays, any_hit)
     assert np.array_equal(got, ref)
-    if kernel != "k_trace_w":
+    if not kernel.startswith("k_trace_w"):
         assert (nodes, prims) == (rnodes, rprims)
 
 
@@ -273,7 +276,8 @@ def test_tile_groups_batching_equal(variant):
 @pytest.mark.parametrize("env", [{"PT_STACK_ROWS": "2"}, {"PT_TRACE_PERSIST": "0"}, {"PT_TRACE_PERSIST": "1"},
                                  {"PT_TRACE_PERSIST": "2"}, {"PT_TRACE_LDS": "0"},
                                  {"PT_TRACE_LDS": "0", "PT_TRACE_PERSIST": "2"}, {"PT_TRACE_OCT": "1"},
-                                 {"PT_TRACE_WIDE": "0"}, {"PT_LEAF_MIN_W": "1"}, {"PT_LEAF_MIN_W": "64"}])
+                                 {"PT_TRACE_WIDE": "0"}, {"PT_LEAF_MIN_W": "1"}, {"PT_LEAF_MIN_W": "64"},
+                                 {"PT_TRACE_LDS": "0", "PT_WIDE_LDS_ROWS": "2"}])
 def test_trace_variants_bit_exact(variant, monkeypatch, env):
     """Every traversal variant the driver can pick -- LDS stack with global
     spill (forced by a 2-entry LDS stack), the non-persistent kernel, the

@@ -114,7 +114,14 @@ def _tie_rays(n_rand, seed, any_hit):
 
 
 @pytest.mark.parametrize("any_hit", [False, True])
-def test_wide_traversal_ties_match_oracle(tmp_path, any_hit):
+@pytest.mark.parametrize("where", ["lds", "hbm"])
+def test_wide_traversal_ties_match_oracle(tmp_path, monkeypatch, any_hit, where):
+    """where: the wide image and primitives staged in LDS (k_trace_w<false>) or
+    read from HBM (k_trace_w<true>, PT_TRACE_LDS=0; with a 2-row LDS stack so
+    the spill column is exercised)."""
+    if where == "hbm":
+        monkeypatch.setenv("PT_TRACE_LDS", "0")
+        monkeypatch.setenv("PT_WIDE_LDS_ROWS", "2")
     hs = ptgpu.HostScene(_tie_scene(tmp_path))
     sc = ptgpu.Scene(hs)
     assert sc.kernel_names()[0] == "k_trace_w"
@@ -166,10 +173,13 @@ def test_wide_tie_scene_render_matches_oracle(tmp_path):
 
 @pytest.mark.parametrize("scene", ["portal_cornell.pbrt", "portal_room.pbrt", "cornell_dielectric.pbrt",
                                    "cornell_dielectric_hero.pbrt"])
-def test_counting_frame_reference_counters(tmp_path, scene):
+@pytest.mark.parametrize("where", ["lds", "hbm"])
+def test_counting_frame_reference_counters(tmp_path, monkeypatch, scene, where):
     """The default render (k_trace_w) and the counting frame (binary traversal in
     the reference's order) give the oracle's image bit for bit; the counting
     frame also the reference's node-visit / primitive-test counters."""
+    if where == "hbm":
+        monkeypatch.setenv("PT_TRACE_LDS", "0")
     path = scene_variant(tmp_path, name=scene, res=(48, 32), spp=8)
     hs = ptgpu.HostScene(path)
     sc = ptgpu.Scene(hs)
@@ -181,7 +191,7 @@ def test_counting_frame_reference_counters(tmp_path, scene):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert_counters(gst, rst, keys)
     sc.set_count_bytes(True)
-    assert sc.kernel_names()[0] == "k_trace_lds"
+    assert sc.kernel_names()[0] == ("k_trace_lds" if where == "lds" else "k_trace_nb")
     got2, gst2 = sc.render()
     assert gst2["trace_wide"] == 0 and gst2["retraced_rays"] == 0
     assert np.array_equal(got2.view(np.uint32), ref.view(np.uint32))
