@@ -69,6 +69,16 @@ constexpr uint32_t kPrimInfoTable = 8u;   // material / area light too large for
 // (bits 0-15) and area light + 1 (bits 16-31), so a hit needs no triangle
 // table or vertex-array load unless the mesh has uv / normals / tangents.
 constexpr uint32_t kPrimTriShift = 8u;
+// Bits 16-17 of word 0 .w: the material's lobe class (k_shade_sort groups the path queue by it): 0 matte / none /
+// no material (and misses), 1 specular lobes only (mirror, smooth glass), 2 microfacet lobes (metal, plastic, rough
+// glass)
+constexpr uint32_t kPrimClassShift = 16u;
+__host__ __device__ constexpr uint32_t material_class(int kind, bool specular) {
+    return (kind == PT_MAT_METAL || kind == PT_MAT_PLASTIC) ? 2u
+           : kind == PT_MAT_MIRROR                          ? 1u
+           : (kind == PT_MAT_GLASS || kind == PT_MAT_DISPERSIVE_GLASS) ? (specular ? 1u : 2u)
+                                                                       : 0u;
+}
 __host__ __device__ constexpr uint32_t prim_info_word(int material, int light) {
     return (uint32_t)(material & 0xffff) | ((uint32_t)(light + 1) << 16);
 }

@@ -1292,8 +1292,10 @@ __device__ __forceinline__ WideHit2 wide_box2(pt_f2 nx, pt_f2 fx, pt_f2 ny, pt_f
     return r;
 }
 
+// wide-node steps per loop iteration for lanes that stay in node mode (C2: 1 / 2 / 3 -> 8.88 / 8.54 / 8.39 ms
+// per launch)
 #ifndef PT_WNODE_STEPS
-#define PT_WNODE_STEPS 2
+#define PT_WNODE_STEPS 3
 #endif
 constexpr int kWNodeSteps = PT_WNODE_STEPS;
 // 6 waves per SIMD (80 VGPRs, no scratch; the compiler's own choice is 82 = 5 waves, and 7 waves spill 40 B)
@@ -2385,6 +2387,79 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         if (lane_id() == 0 && abw) atomicAdd(&stats->shade_bytes, abw);
     }
 }
+
+// ----------------------------------------------------------------------------
+// k_shade_sort (round 6): the path queue grouped by the material class of each
+// path's new hit (kPrimClassShift: matte, specular, microfacet; misses and
+// paths with only an NEE resolve pending count as matte), chunk by chunk:
+// block b takes entries [4096 b, 4096 (b + 1)) and writes them back to the
+// same range with the classes one after the other.  The shading kernel's
+// waves take 64 consecutive entries, so almost every wave then holds one class
+// and its material branches (make_bsdf, the lobe loops of BSDF::f / Pdf /
+// Sample_f) are uniform: a matte wave no longer executes FresnelSpecular or
+// the microfacet lobes because one of its lanes hit glass.  Paths are
+// independent, so the order of a queue never changes a result.
+// ----------------------------------------------------------------------------
+constexpr uint32_t kSortChunk = 4096;  // 256 threads x 16 entries
+__global__ __launch_bounds__(256) void k_shade_sort(DevScene sc, DevPaths ps, const uint32_t* __restrict__ pq,
+                                                    const uint32_t* __restrict__ pq_count, uint32_t* __restrict__ out)
+#ifdef PT_TU_MISC
+{
+    __shared__ uint32_t buf[kSortChunk];
+    __shared__ uint32_t cnt[3], run[3];
+    const uint32_t n = *pq_count;
+    const uint32_t c0 = blockIdx.x * kSortChunk;
+    if (c0 >= n) return;
+    const uint32_t m = min(kSortChunk, n - c0);
+    if (threadIdx.x < 3) { cnt[threadIdx.x] = 0; run[threadIdx.x] = 0; }
+    __syncthreads();
+    uint32_t slot[16], cls = 0;  // cls: 2 bits per entry, 3 = none
+    const uint32_t lane = lane_id();
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t i = (uint32_t)k * 256u + threadIdx.x;
+        uint32_t c = 3;
+        slot[k] = 0;
+        if (i < m) {
+            const uint32_t s = pq[c0 + i];
+            slot[k] = s;
+            const uint32_t stw = *st_word(ps, s);
+            const int h = *hit_word(ps, s, kHdHit);
+            c = ((stw & kStCont) && h >= 0) ? (__float_as_uint(sc.prims[3 * h].w) >> kPrimClassShift) & 3u : 0u;
+            c = c > 2 ? 0 : c;
+        }
+        cls |= c << (2 * k);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // per-class counts: one LDS atomic per wave and class
+        const uint32_t c = (cls >> (2 * k)) & 3u;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; ++q) {
+            const uint32_t nq = (uint32_t)__popcll(__ballot(c == q));
+            if (lane == 0 && nq) atomicAdd(&cnt[q], nq);
+        }
+    }
+    __syncthreads();
+    const uint32_t off1 = cnt[0], off2 = cnt[0] + cnt[1];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // positions: the class's offset + the wave's block of it + the lane's rank
+        const uint32_t c = (cls >> (2 * k)) & 3u;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; ++q) {
+            const uint64_t b = __ballot(c == q);
+            uint32_t base = 0;
+            if (lane == 0 && b) base = atomicAdd(&run[q], (uint32_t)__popcll(b));
+            base = __builtin_amdgcn_readlane(base, 0);
+            if (c == q) buf[(q == 0 ? 0u : (q == 1 ? off1 : off2)) + base + (uint32_t)__popcll(b & below)] = slot[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += 256) out[c0 + i] = buf[i];
+}
+#else
+;
+#endif
 
 // ----------------------------------------------------------------------------
 // DirectLightingIntegrator::Li (directlighting.cpp:58-84) as a resumable

@@ -166,6 +166,7 @@ constexpr int kMaxPipes = 4;  // render_tiles pipelines (PT_PIPES)
 struct Work {
     DBuf<uint32_t> rq0, rq1, pq0, pq1, counts;
     DBuf<uint32_t> rqr;  // k_trace_w: ray-queue entries handed to the binary traversal (counts[6])
+    DBuf<uint32_t> pqs;  // k_shade_sort: the path queue grouped by material class per chunk
     DBuf<uint4> head;   // DevPaths records (device.h)
     DBuf<float4> body;
     DBuf<float2> pfilm;
@@ -211,7 +212,7 @@ struct Work {
             dl_frames = frames;
         }
         if (n > cap) {
-            rq0.alloc(3 * n); rq1.alloc(3 * n); rqr.alloc(3 * n); pq0.alloc(n); pq1.alloc(n);
+            rq0.alloc(3 * n); rq1.alloc(3 * n); rqr.alloc(3 * n); pq0.alloc(n); pq1.alloc(n); pqs.alloc(n);
             head.alloc(n); body.alloc(2 * n); pfilm.alloc(n); ray.alloc(8 * n); rayA.alloc(8 * n);
             rayB.alloc(8 * n); nee.alloc((size_t)kNee * n); Lfin.alloc(3 * n);
             cap = n;
@@ -295,6 +296,10 @@ struct pt_scene {
     size_t wide_lds_bytes = 0;   // > 0: k_trace_w, its dynamic LDS (PT_TRACE_WIDE=0 disables): LDS-resident scenes the
                                  // 4-wide BVH image + primitive records + stack, HBM-resident ones the stack rows
     bool wide_hbm = false;       // k_trace_w<true>: the wide image and the primitives from HBM
+    uint32_t mat_classes = 1;    // material classes among the primitives (bit c: kPrimClassShift class c present)
+    bool shade_sort = false;     // PT_SHADE_SORT=1: k_shade_sort before the path integrator's shading when 2+ classes
+                                 // (C3 @256: 424.8 vs 452.6 Msamples/s without -- the queue order from the pixel-major
+                                 // batches keeps most waves one class already)
     int wide_rows = 0;           // k_trace_w stack rows per lane (dummy row + deepest stack + 3 push rows)
     int wide_lds_rows = 0;       // of them in LDS (k_trace_w<true>: the rest in the lane's spill column)
     int leaf_min_w = 48;         // k_trace_w: lanes parked at leaves that trigger a primitive-test step (PT_LEAF_MIN_W;
@@ -718,6 +723,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     }
     auto Pv = [&](int k) { return v3(d->P[3 * k], d->P[3 * k + 1], d->P[3 * k + 2]); };
     std::vector<float4> prims(3 * s->host_prim_order.size());
+    uint32_t class_mask = 1u;  // material classes among the primitives (misses: class 0)
     for (size_t i = 0; i < s->host_prim_order.size(); ++i) {
         const pt_prim& p = d->prims[s->host_prim_order[i]];
         uint32_t flags = 0;
@@ -755,6 +761,11 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
             }
         }
         prims[3 * i + 1] = make_float4(b.x, b.y, b.z, __builtin_bit_cast(float, p.index));
+        if (pmat >= 0 && pmat < d->n_materials) {
+            const uint32_t mc = material_class(d->materials[pmat].kind, d->materials[pmat].specular != 0);
+            flags |= mc << kPrimClassShift;
+            class_mask |= 1u << mc;
+        }
         uint32_t info = 0;
         if (prim_info_fits(pmat, plight)) info = prim_info_word(pmat, plight);
         else flags |= kPrimInfoTable;
@@ -763,6 +774,7 @@ static void build_scene(pt_scene* s, const pt_scene_desc* d, const pt_scene* bvh
     }
     s->nodes.upload(nodes);
     s->prims.upload(prims);
+    s->mat_classes = class_mask;
     s->tris.upload(d->triangles, (size_t)d->n_triangles);
     s->P.upload(d->P, (size_t)3 * d->n_vertices);
     if (d->N) s->N.upload(d->N, (size_t)3 * d->n_vertices);
@@ -1442,8 +1454,15 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     const ShadeKernel kshade =
                         direct ? k_shade_dl<kFtAll>
                                : shade_kernel(shade_variant_of(s), s->features, s->count_bytes);
+                    // scenes with two or more material classes: the path queue grouped by class per 4096-entry
+                    // chunk first, so a shading wave's paths mostly take one BSDF's code (k_shade_sort)
+                    const bool sorted = !direct && s->shade_sort && __builtin_popcount(s->mat_classes) > 1;
+                    if (sorted)
+                        hipLaunchKernelGGL(k_shade_sort, dim3(std::max(1, ceil_div(npaths, kSortChunk))), dim3(256), 0,
+                                           st, s->dev, ps, pq_in, counts + 1, w.pqs.p);
                     hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
-                                       pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3, w.stats.p);
+                                       sorted ? w.pqs.p : pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3,
+                                       w.stats.p);
                 }
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(es.second, st));
@@ -1899,6 +1918,7 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     if (const char* t = std::getenv("PT_LEAF_MIN")) s->leaf_min = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_LEAF_MIN_PT")) s->leaf_min_pt = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("PT_BATCH_EQUAL")) s->batch_equal = std::max(0, std::atoi(t));
+    if (const char* t = std::getenv("PT_SHADE_SORT")) s->shade_sort = t[0] != '0';
     if (const char* t = std::getenv("PT_PIPES")) s->pipes = std::max(1, std::min(kMaxPipes, std::atoi(t)));
     return s;
 }

@@ -299,6 +299,7 @@ SHADE_VARIANTS = [
     {"PT_SHADE_VARIANT": "5", "PT_SHADE_TAB": "0"},
     {"PT_SHADE_VARIANT": "4"},                          # k_shade_w3h: 3 waves, scene tables from HBM
     {"PT_SHADE_TAB": "0"},                              # default without table room (C5: k_shade_w3h if portal-only)
+    {"PT_SHADE_SORT": "1"},                             # the path queue grouped by material class (k_shade_sort)
 ]
 
 
