@@ -117,11 +117,21 @@ def _heartbeat(period: float = 30.0) -> None:
     threading.Thread(target=beat, daemon=True).start()
 
 
-def cpu_baseline(scene_path: str, seconds: float, hs=None):
+# Frames of more than this many samples per pixel (C5 as written: 4096) take the CPU baseline, the parity
+# check and the isolated / counting frames on the first CPU_SPP_CAP samples of every pixel (a bounded sample of
+# the same frame: Halton indices [0, cap), HaltonSampler::StartPixelSample order) -- a full-spp CPU tile alone
+# would run for minutes
+CPU_SPP_CAP = 1024
+CPU_SPP_SAMPLE = 64
+ISO_SPP_SAMPLE = 16
+
+
+def cpu_baseline(scene_path: str, seconds: float, hs=None, spp_cap: int = 0):
     """Reference CPU path restated in C (oracle/, 'port'), timed on this host's
     cores on a bounded sample of the same frame: the 16x16 tiles t with
     t % stride == 0, spread over the whole image (stride sized so the timed
-    run takes about `seconds`)."""
+    run takes about `seconds`), all samples of each pixel, or its first
+    `spp_cap` (> 0) for the frames above CPU_SPP_CAP spp."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import ptgpu
@@ -136,16 +146,21 @@ def cpu_baseline(scene_path: str, seconds: float, hs=None):
     w, h = hs.film_size()
     ntiles = ((w + 15) // 16) * ((h + 15) // 16)
     stride = max(1, ntiles // (2 * threads))
+    def oracle_tiles(stride_):
+        if spp_cap > 0:
+            return pyoracle.render_range(hs.desc, 0, spp_cap, nthreads=threads, tile_offset=0, tile_stride=stride_)
+        return pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride_)
+
     _progress(f"cpu baseline: calibration run (tile stride {stride}, {threads} threads)")
     t0 = time.perf_counter()
-    _, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
+    _, st = oracle_tiles(stride)
     dt = time.perf_counter() - t0
     per_tile = st["samples"] / max(1, (ntiles + stride - 1) // stride)
     want = max(2 * threads, min(ntiles, st["samples"] / dt * seconds / per_tile))
     stride = max(1, int(ntiles // want))
     _progress(f"cpu baseline: timed run (tile stride {stride})")
     t0 = time.perf_counter()
-    film, st = pyoracle.render_accum(hs.desc, nthreads=threads, tile_offset=0, tile_stride=stride)
+    film, st = oracle_tiles(stride)
     dt = time.perf_counter() - t0
     rate = st["samples"] / dt / 1e6
     host = os.cpu_count() or threads
@@ -156,7 +171,8 @@ def cpu_baseline(scene_path: str, seconds: float, hs=None):
                              + f"; the host has {host} CPUs"),
             "all_host_cpus_linear_estimate": round(rate / threads * host, 3),
             "sample": f"every {stride}th 16x16 tile of the same frame (tiles t % {stride} == 0 over the whole image) "
-                      f"at the scene's spp ({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
+                      + (f"at the first {spp_cap} samples of each pixel" if spp_cap > 0 else "at the scene's spp")
+                      + f" ({st['samples']} samples, {dt:.1f} s, {threads} threads; oracle/pt_oracle.c)",
             "mrays_per_s": round((st["closest_rays"] + st["shadow_rays"]) / dt / 1e6, 3),
             "per_thread": round(rate / threads, 4),
             "reference_probe": dict(REFERENCE_PROBE, per_thread=round(REFERENCE_PROBE["value"] / 8, 4))}, \
@@ -356,18 +372,21 @@ def rooflines(timed: dict, iso: dict, workload: str, config: str, lds_scene: boo
     return {"roofline": roof, "roofline_kernels": ks}
 
 
-def parity_check(sc, hs, stride: int, ref_acc, ref_st: dict) -> dict:
+def parity_check(sc, hs, stride: int, ref_acc, ref_st: dict, spp_cap: int = 0) -> dict:
     """The GPU film of the tiles t % stride == 0 (the cpu_baseline's sample of
     the same frame), rendered with the production batch size and pipelines,
     against the oracle's film of the same tiles: bit-exact pixels of the film
     (XYZ + weight, Film::Pixel), RMSE of the resolved image, and the
     reference's ray / node / primitive counters (integrator.cpp:526-637)."""
     import numpy as np
-    got, gst = sc.render_accum(0, stride)
+    def tiles():  # the same tiles (and sample range) as the cpu_baseline leg
+        return sc.render_range(0, spp_cap, 0, stride) if spp_cap > 0 else sc.render_accum(0, stride)
+
+    got, gst = tiles()
     # the counting frame's traversal (binary, the reference's visit order) for the node / primitive counters,
     # which the 4-wide k_trace_w does not reproduce; its film must be bit-exact too
     sc.set_count_bytes(True)
-    got_c, gst_c = sc.render_accum(0, stride)
+    got_c, gst_c = tiles()
     sc.set_count_bytes(False)
     same_c = bool(np.array_equal(got_c.view(np.uint32), ref_acc.view(np.uint32)))
     same = np.all(got.view(np.uint32) == ref_acc.view(np.uint32), axis=2)
@@ -377,7 +396,8 @@ def parity_check(sc, hs, stride: int, ref_acc, ref_st: dict) -> dict:
     rmse = float(np.sqrt(np.mean((a - b) ** 2)))
     keys = ("samples", "closest_rays", "shadow_rays")
     order_keys = ("node_visits", "prim_tests")
-    return {"tiles": f"t % {stride} == 0", "samples": int(gst["samples"]),
+    return {"tiles": f"t % {stride} == 0" + (f", samples [0, {spp_cap})" if spp_cap > 0 else ""),
+            "samples": int(gst["samples"]),
             "bit_exact_pixels": round(float(np.mean(same)), 6),
             "bit_exact_rendered_pixels": round(float(np.mean(same[touched])), 6) if touched.any() else None,
             "rendered_pixels": int(touched.sum()), "rmse": rmse,
@@ -492,10 +512,15 @@ def main():
     iso = {"trace_ms": 0.0, "trace_launches": 0, "shade_ms": 0.0, "shade_launches": 0, "shade_bytes": 0,
            "node_visits": 0, "prim_tests": 0, "wide_node_visits": 0, "wide_prim_tests": 0, "retraced_rays": 0}
     _progress("isolated and byte-counting frames")
+    # above CPU_SPP_CAP spp (C5 as written, 4096) both extra frames render the first ISO_SPP_SAMPLE samples of
+    # every pixel: per-launch figures from the same batches, bounces and launches in both
+    import dataclasses
+    iso_shard = my if spp <= CPU_SPP_CAP else dataclasses.replace(
+        my, sample_end=min(my.sample_end, my.sample_begin + ISO_SPP_SAMPLE))
     pipes = sc.query("pipelines")
     sc.set_pipelines(1)
     accum.zero_()
-    st = render(my)
+    st = render(iso_shard)
     torch.cuda.synchronize()
     sc.set_pipelines(pipes)
     for k in iso:
@@ -506,7 +531,7 @@ def main():
     # register: a separate instantiation, pt_set_count_bytes; the same batches, bounces and launches)
     sc.set_count_bytes(True)
     accum.zero_()
-    st = render(my)
+    st = render(iso_shard)
     torch.cuda.synchronize()
     sc.set_count_bytes(False)
     iso["shade_bytes"], iso["shade_launches_counted"] = st["shade_bytes"], st["shade_launches"]
@@ -555,11 +580,13 @@ def main():
         out["source_hash"] = src
         out.update(rooflines(agg, iso, workload, args.config, lds_scene, names, src,
                              ms_per_step=round(dt / args.steps * 1e3, 2)))
+        out["isolated_frame_spp"] = iso_shard.samples_per_pixel
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds, hs)
+            cap = CPU_SPP_SAMPLE if spp > CPU_SPP_CAP else 0
+            out["cpu_baseline"], (stride, ref_acc, ref_st) = cpu_baseline(spath, args.cpu_seconds, hs, cap)
             if not args.no_parity:
                 _progress("parity: the sampled tiles on the GPU")
-                out["parity"] = parity_check(sc, hs, stride, ref_acc, ref_st)
+                out["parity"] = parity_check(sc, hs, stride, ref_acc, ref_st, cap)
         if emul is not None:
             out["emulated_scaling"] = emul
         print(json.dumps(out), flush=True)
