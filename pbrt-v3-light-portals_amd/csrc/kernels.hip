@@ -2025,10 +2025,18 @@ struct PathNow {
     PrimRec rec;
 };
 template <int kFt>
+__device__ __forceinline__ void path_load_nee(const DevPaths& ps, uint32_t slot, const PathPre& p, PathNow* q) {
+    if (p.st & kStNee) q->nee = nee_load<Ft<kFt>::mis>(ps, slot, (p.st & kStNfMask) >> kStNfShift, p.hitA);
+}
+template <int kFt>
+__device__ __forceinline__ void path_load_rec(const DevScene& sc, const PathPre& p, PathNow* q) {
+    if ((p.st & kStCont) && p.hit >= 0) q->rec = prim_rec(sc, p.hit);
+}
+template <int kFt>
 __device__ __forceinline__ void path_load_now(const DevScene& sc, const DevPaths& ps, uint32_t slot, const PathPre& p,
                                               PathNow* q) {
-    if (p.st & kStNee) q->nee = nee_load<Ft<kFt>::mis>(ps, slot, (p.st & kStNfMask) >> kStNfShift, p.hitA);
-    if ((p.st & kStCont) && p.hit >= 0) q->rec = prim_rec(sc, p.hit);
+    path_load_nee<kFt>(ps, slot, p, q);
+    path_load_rec<kFt>(sc, p, q);
 }
 // Two stages: the head record (state word with the payload flags, hits) two
 // paths ahead, the body one path ahead and only what the head says this step
@@ -2255,19 +2263,24 @@ __device__ __forceinline__ DevScene stage_tables(const DevScene& sc, uint4* lds)
 // register, which the 3-wave build cannot spare, so the counting build is a
 // separate instantiation that the renderer runs only on request
 // (pt_set_count_bytes; the bench's one extra frame).
-// kAhead: the NEE payload and the hit primitive's record (path_load_now) are
+// kAhead 2: the NEE payload and the hit primitive's record (path_load_now) are
 // loaded one path ahead as well, with the next path's body, instead of at the
 // start of the path's own step -- ≈30 more VGPRs, for the 2-wave MIS kernels
-// whose feature set leaves them (ShadeAhead)
+// whose feature set leaves them (ShadeAhead); kAhead 1: the payload alone one
+// path ahead, the record at the step's start (the two-lobe sets, C3)
 #define PT_ABP (kAb ? &ab : nullptr)
 #ifdef PT_NO_AHEAD  // experiment build: the round-4 order
 template <int kFt>
-constexpr bool kShadeAhead = false;
+constexpr int kShadeAhead = 0;
 #else
-template <int kFt>
-constexpr bool kShadeAhead = Ft<kFt>::mis && !(Ft<kFt>::micro && Ft<kFt>::spec);  // two-lobe sets: 256 VGPRs, one wave
+// two-lobe sets: 256 VGPRs and one wave with both ahead; the payload alone ahead fits 2 waves (PT_AHEAD1=0: off)
+#ifndef PT_AHEAD1
+#define PT_AHEAD1 1
 #endif
-template <int kFt, bool kTab, bool kLean = false, bool kAb = false, bool kAhead = false>
+template <int kFt>
+constexpr int kShadeAhead = !Ft<kFt>::mis ? 0 : (!(Ft<kFt>::micro && Ft<kFt>::spec) ? 2 : PT_AHEAD1);
+#endif
+template <int kFt, bool kTab, bool kLean = false, bool kAb = false, int kAhead = 0>
 __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths& ps, const uint32_t* __restrict__ pq,
                                             const uint32_t* __restrict__ pq_count, uint32_t* rq_out,
                                             uint32_t* rq_out_count, uint32_t* pq_out, uint32_t* pq_out_count,
@@ -2346,19 +2359,27 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         path_prefetch_head<Ft<kFt>::mis>(ps, slot1, &nxt);
     }
     if (i0 + 2 * stride < n) slot2 = pq[i0 + 2 * stride];
-    PathNow now{};  // kAhead: this path's NEE payload and hit record, loaded one path ahead
-    if constexpr (kAhead) {
+    PathNow now{};  // kAhead: this path's NEE payload (and hit record), loaded one path ahead
+    if constexpr (kAhead == 2) {
         if (i0 < n) path_load_now<kFt>(sc, ps, slot, pre, &now);
+    } else if constexpr (kAhead == 1) {
+        if (i0 < n) path_load_nee<kFt>(ps, slot, pre, &now);
     }
     for (; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
         PathPre nn{};
         uint32_t slot3 = 0;
         PathNow nowN{};
-        if constexpr (kAhead) {
+        if constexpr (kAhead == 2) {
             if (i + stride < n) {
                 path_prefetch_body(ps, slot1, &nxt);  // its head arrived during the last path
                 path_load_now<kFt>(sc, ps, slot1, nxt, &nowN);
+            }
+        } else if constexpr (kAhead == 1) {
+            if (i < n) path_load_rec<kFt>(sc, pre, &now);  // issued ahead of the prefetches below
+            if (i + stride < n) {
+                path_prefetch_body(ps, slot1, &nxt);
+                path_load_nee<kFt>(ps, slot1, nxt, &nowN);
             }
         } else {
             now = PathNow{};
@@ -2376,7 +2397,7 @@ __device__ __forceinline__ void shade_batch(const DevScene& sc0, const DevPaths&
         slot2 = slot3;
         pre = nxt;
         nxt = nn;
-        if constexpr (kAhead) now = nowN;
+        if constexpr (kAhead != 0) now = nowN;
     }
     }
 #endif
