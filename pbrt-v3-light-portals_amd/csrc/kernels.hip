@@ -376,8 +376,6 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_PT_ATTR void k_trace_pt(DevSc
     static_assert(kTraceBlock * 4 == 512, "k_trace_pt stack rows are 512 bytes apart");
 #define SPILL(v) ((blockIdx.x * (uint32_t)kTraceBlock + ((so & 511u) >> 2)) * 64u + (uint32_t)(v))
 #define STK(o) (*reinterpret_cast<int*>(reinterpret_cast<char*>(stk) + (o)))
-    // per lane per launch: nodes / prims fit 32 bits, rays 16 bits each (closest | shadow << 16); the loop
-    // count is the wave's (uniform, a scalar register)
     // The counters as wave totals (uniform: scalar registers).  A lane's node visits and primitive tests of
     // one loop iteration (cst: visits in bits 0-3, tests in bits 8-11) are added at the top of the next,
     // where the wave's lanes are converged, one ballot per bit; rays where the refill takes them.

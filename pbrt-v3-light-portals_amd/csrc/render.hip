@@ -278,7 +278,7 @@ struct pt_scene {
     int pipes = 2;                 // pipelines render_tiles runs batches on (PT_PIPES)
     int device = 0;
     int num_cus = 256;
-    size_t target_slots = 0;  // batch size in camera samples; 0: 96 M (8 M for the 60-bin hero state)
+    size_t target_slots = 0;  // batch size in camera samples; 0: 96 M (32 M for the 60-bin hero state)
     int dl_max_samples = 1;      // DirectLighting: largest Light::nSamples
     size_t lds_scene_bytes = 0;  // > 0: k_trace stages the BVH in LDS
     size_t hal_lds_bytes = 0;    // dynamic LDS of k_shade: the staged Halton tables (DevScene::hal_lds_dims)
@@ -1293,9 +1293,9 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
         int bx0, by0, bx1, by1;
     };
     std::vector<Group> groups;
-    // 96 M camera samples (C2: 64 M 877, 96 M 897, 128 M 896, 160 M 896 Msamples/s, same box)
-    // default batches: 96 M camera samples, 32 M for the hero integrators (1.2 KB of path state per slot:
-    // 38 GB per pipeline; C3h 8 / 16 / 32 / 64 M: 107.0 / 109.1 / 110.1 / 110.3 Msamples/s)
+    // default batches: 96 M camera samples (C2: 64 M 877, 96 M 897, 128 M 896, 160 M 896 Msamples/s, same box),
+    // 32 M for the hero integrators (1.2 KB of path state per slot: 38 GB per pipeline; C3h 8 / 16 / 32 / 64 M:
+    // 107.0 / 109.1 / 110.1 / 110.3 Msamples/s)
     size_t target = s->target_slots ? s->target_slots : (s->hero ? (size_t)32 << 20 : (size_t)96 << 20);
     {   // a render of only a few batches (one rank's shard of a multi-GPU frame) is split into equal batches, a
         // multiple of the pipelines, so the pipelines finish together instead of one running a short remainder
@@ -1460,7 +1460,12 @@ static RenderResult render_tiles(pt_scene* s, int offset, int stride, int s_begi
                     if (sorted)
                         hipLaunchKernelGGL(k_shade_sort, dim3(std::max(1, ceil_div(npaths, kSortChunk))), dim3(256), 0,
                                            st, s->dev, ps, pq_in, counts + 1, w.pqs.p);
-                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), direct ? 0 : s->hal_lds_bytes, st, s->dev, ps,
+                    // dynamic LDS: the Halton tables, + the scene tables for the builds that stage them (variants 3
+                    // and 5; k_shade and k_shade_w3h read the tables from HBM: ds.hal_lds_bytes alone)
+                    const int sv = shade_variant_of(s);
+                    const size_t shade_lds = direct ? 0 : ((sv == 3 || sv == 5) ? s->hal_lds_bytes
+                                                                                   : (size_t)s->dev.hal_lds_bytes);
+                    hipLaunchKernelGGL(kshade, sg, dim3(kShadeBlock), shade_lds, st, s->dev, ps,
                                        sorted ? w.pqs.p : pq_in, counts + 1, rq_out, counts + 2, pq_out, counts + 3,
                                        w.stats.p);
                 }

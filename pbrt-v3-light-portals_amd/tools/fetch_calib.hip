@@ -32,7 +32,7 @@
         }                                                                                         \
     } while (0)
 
-constexpr uint32_t kLog2Slots = 26;  // 64 M slots, as the default shading batch
+constexpr uint32_t kLog2Slots = 26;  // 64 M slots (the default shading batch when calibrated in round 5; 96 M since)
 constexpr uint32_t kSlots = 1u << kLog2Slots;
 
 __device__ __forceinline__ uint32_t perm(uint32_t i, bool rnd) {
