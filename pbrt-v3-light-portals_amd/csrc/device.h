@@ -274,6 +274,10 @@ constexpr int kNeeSw = 11;     // MIS scattering weight
 constexpr int kNeeSpdf = 12;   // MIS scattering pdf                                 | quarter 3
 constexpr int kNeePortalPdf = 13;
 constexpr int kNeeLight = 14;  // light index (int bits)
+// the shading step writes whole quarters ({beta, lpdf} {F, pdf} {Li, sw} {spdf, portal pdf, light, -})
+static_assert(kNeeBeta == 0 && kNeeLpdf == 3 && kNeeF == 4 && kNeePdf == 7 && kNeeLi == 8 && kNeeSw == 11 &&
+                  kNeeSpdf == 12 && kNeePortalPdf == 13 && kNeeLight == 14,
+              "payload quarters");
 
 constexpr uint32_t kNfPortal = 1u;     // portal-light estimator (ray A closest)
 constexpr uint32_t kNfMis = 2u;        // standard MIS (ray A shadow, ray B closest)

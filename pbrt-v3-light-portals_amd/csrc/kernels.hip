@@ -1553,11 +1553,13 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_W_ATTR void k_trace_w(DevScen
                         else if (srow(a) < (uint32_t)kSpillWords) PT_SCOL[srow(a)] = v;
                     }
                 }
-                const bool empty = sp == sbase;
-                const bool pop = (nh == 0) & !empty;
-                const uint32_t nxt = nh == 0 ? top : (nh == 1 ? w0 : (nh == 2 ? w1 : (nh == 3 ? w2 : w3)));
-                sp = nh > 0 ? sp + 512u * (nh - 1u) : (pop ? sp - 512u : sp);
-                const bool go = (nh > 0) | pop;
+                // the nearest hit w[nh - 1] (or the popped top) as three selects: the compiler turned the
+                // nested conditional into branches (-13 SALU and 2 branches per node step)
+                const bool go = (nh > 0) | (sp != sbase);
+                const uint32_t s01 = nh >= 2u ? w1 : w0, s23 = nh >= 4u ? w3 : w2;
+                const uint32_t sn = nh >= 3u ? s23 : s01;
+                const uint32_t nxt = nh == 0u ? top : sn;
+                sp = nh > 0 ? sp + 512u * (nh - 1u) : (go ? sp - 512u : sp);
                 const bool inner = go & ((int)nxt < 0);
                 const bool leaf = go & ((int)nxt >= 0);
                 nm = inner;
@@ -1837,6 +1839,11 @@ __device__ __forceinline__ void put_nee(const DevPaths& ps, uint32_t slot, int k
 __device__ __forceinline__ void put_nee3(const DevPaths& ps, uint32_t slot, int k, S3 v) {
     put_nee(ps, slot, k, v.c[0]); put_nee(ps, slot, k + 1, v.c[1]); put_nee(ps, slot, k + 2, v.c[2]);
 }
+// one whole 16-B quarter of the payload record in one store (a 4-B store per field made a portal
+// step's payload nine store instructions, each addressing 64 lanes' records)
+__device__ __forceinline__ void put_nee_q(const DevPaths& ps, uint32_t slot, int q, S3 v, float w) {
+    reinterpret_cast<float4*>(ps.nee)[4u * slot + (uint32_t)q] = make_float4(v.c[0], v.c[1], v.c[2], w);
+}
 
 // PortalArealight::EstimateDirect set-up (portal_arealight.cpp:29-239).
 // u1 = uScattering (argument order at integrator.cpp:132); u2 is unused; the
@@ -1920,8 +1927,7 @@ __device__ __forceinline__ uint32_t portal_nee(const DevScene& sc, const DevPath
                 if (pdf > 0) {
                     const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
                     store_ray(ps.rayA, slot, r);
-                    put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
-                    put_nee(ps, slot, kNeePdf, pdf);
+                    put_nee_q(ps, slot, kNeeF / 4, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn), pdf);
                     // Li = 0 before the portal ray is traced (portal_arealight.cpp:181), kept on a miss: a flag
                     // instead of a 12-B store and load
                     flags |= kNfA | kNfLi0;
@@ -1938,9 +1944,8 @@ __device__ __forceinline__ uint32_t portal_nee(const DevScene& sc, const DevPath
     if (!is_black(Li) && pdf > 0) {
         const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi), wi, kInf};
         store_ray(ps.rayA, slot, r);
-        put_nee3(ps, slot, kNeeF, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn));
-        put_nee(ps, slot, kNeePdf, pdf);
-        put_nee3(ps, slot, kNeeLi, Li);
+        put_nee_q(ps, slot, kNeeF / 4, bsdf_f<kFt>(bsdf, it.wo, wi, kBxNonSpecular) * absdot(wi, it.sn), pdf);
+        put_nee_q(ps, slot, kNeeLi / 4, Li, 0.f);  // .w: the MIS weight's word, unread by the portal resolve
         flags |= kNfA;
         if (ab) *ab += 24 + 12 + 4 + 12;
     }
@@ -1968,10 +1973,10 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
             const V3 d = target - origin;
             store_ray(ps.rayA, slot, Ray{origin, d, 1 - kShadowEps});
             if (l.kind == PT_LIGHT_POINT) {  // IsDeltaLight: no MIS weight (integrator.cpp:186-188)
-                put_nee3(ps, slot, kNeeF, (f * Li) / lightPdf);
+                put_nee_q(ps, slot, kNeeF / 4, (f * Li) / lightPdf, 0.f);  // .w: the portal pdf's word, unread
             } else {
                 const float lightWeight = power_heuristic(lightPdf, scatteringPdf);
-                put_nee3(ps, slot, kNeeF, ((f * Li) * lightWeight) / lightPdf);
+                put_nee_q(ps, slot, kNeeF / 4, ((f * Li) * lightWeight) / lightPdf, 0.f);
             }
             flags |= kNfA | kNfC1;
             if (ab) *ab += 28 + 12;
@@ -1989,10 +1994,10 @@ __device__ __forceinline__ uint32_t mis_nee(const DevScene& sc, const DevPaths& 
                 const float sw = power_heuristic(pdf2, lp);
                 const Ray r{offset_ray_origin(it.p, it.perr, it.n, wi2), wi2, kInf};
                 store_ray(ps.rayB, slot, r);
-                put_nee3(ps, slot, kNeeLi, f);
-                put_nee(ps, slot, kNeeSw, sw);
-                put_nee(ps, slot, kNeeSpdf, pdf2);
-                put_nee(ps, slot, kNeeLight, __int_as_float(lightIdx));
+                put_nee_q(ps, slot, kNeeLi / 4, f, sw);
+                // {spdf, portal pdf (unread here), light, -}
+                reinterpret_cast<float4*>(ps.nee)[4u * slot + (uint32_t)kNeeSpdf / 4u] =
+                    make_float4(pdf2, 0.f, __int_as_float(lightIdx), 0.f);
                 flags |= kNfB;
                 if (ab) *ab += 24 + 12 + 4 + 4 + 4;
             }
@@ -2163,8 +2168,7 @@ __device__ __forceinline__ void shade_path(const DevScene& sc, const HalLds& hl,
                         }
                     }
                     if (deferred) {
-                        put_nee3(ps, slot, kNeeBeta, beta);
-                        put_nee(ps, slot, kNeeLpdf, lightPdf);
+                        put_nee_q(ps, slot, kNeeBeta / 4, beta, lightPdf);
                         if (ab) *ab += 12 + 4;
                         st = (st & ~kStNfMask) | kStNee | (nf << kStNfShift);
                     } else {

@@ -98,4 +98,4 @@ if has calib; then
     > "$o/cwrite.log" 2>&1
   rc=$?; echo "calib write rc=$rc"; ok $rc cwrite
 fi
-echo "gpu_r5 $OUT done"
+echo "gpu_r6 $OUT done"
