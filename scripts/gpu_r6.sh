@@ -78,6 +78,12 @@ if has sq; then
     --output-format csv -- python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline $SQ \
     > "$o/sq2.log" 2>&1
   rc=$?; echo "pmc sq2 rc=$rc"; ok $rc sq2
+  # VALU lane utilisation: thread-cycles of VALU work against 64 x the VALU instruction cycles
+  timeout -s KILL 150 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS \
+    SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAVES SQ_INSTS_VALU -d "$o/pmc_sq3" -o sq3 \
+    --output-format csv -- python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu-baseline $SQ \
+    > "$o/sq3.log" 2>&1
+  rc=$?; echo "pmc sq3 rc=$rc"; ok $rc sq3
 fi
 if has icache; then
   # instruction-cache hits / misses of the bench's kernels (SQC block), beside the instruction counts

@@ -25,13 +25,16 @@ a = ap.parse_args()
 
 sums = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-for f in glob.glob(os.path.join(a.out, a.glob, "**", "*counter_collection.csv"), recursive=True):
+for f in sorted(glob.glob(os.path.join(a.out, a.glob, "**", "*counter_collection.csv"), recursive=True)):
+    part = collections.defaultdict(lambda: collections.defaultdict(float))  # this pass's sums
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         if not ("k_shade" in k or "k_trace" in k or "k_film" in k or "k_camera" in k):
             continue
-        sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        part[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", ""))
+    for k, c in part.items():  # a counter collected in several passes: the later pass's sum
+        sums[k].update(c)
 
 src = a.source_hash
 if not src and os.path.exists(os.path.join(a.out, "source_hash.txt")):
@@ -42,7 +45,7 @@ if not src:
     import bench
     src = bench.source_hash()
 out = {"workload": a.workload, "config": a.config, "source_hash": src, "bench_args": a.args,
-       "method": "rocprofv3 --pmc, two passes of 8 SQ counters each (scripts/gpu_r4.sh (stage sq)); sums over dispatches",
+       "method": "rocprofv3 --pmc, passes of 8 SQ counters each (scripts/gpu_r6.sh stage sq); sums over dispatches; counters in two passes (SQ_WAVES, SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU) keep the last pass's value",
        "kernels": {}}
 for k, c in sums.items():
     w = c.get("SQ_WAVES", 0) or 1
@@ -51,6 +54,9 @@ for k, c in sums.items():
     e["wait_any_share"] = c.get("SQ_WAIT_ANY", 0) / cyc
     e["wait_inst_any_share"] = c.get("SQ_WAIT_INST_ANY", 0) / cyc
     e["active_inst_any_share"] = c.get("SQ_ACTIVE_INST_ANY", 0) / cyc
+    if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+        # rocprofv3's VALUUtilization: active lanes per VALU instruction cycle, of 64
+        e["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
     for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM"):
         if n in c:
             e[n.replace("SQ_INSTS_", "insts_per_wave_").lower()] = c[n] / w
