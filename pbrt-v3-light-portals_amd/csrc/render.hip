@@ -1820,11 +1820,6 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
     const char* e = std::getenv("PT_TRACE_LDS");
     s->lds_scene_bytes = (scene_bytes > 0 && scene_bytes <= (size_t)kLdsSceneMax && !(e && e[0] == '0'))
                              ? scene_bytes : 0;
-    // A BVH traversed from HBM (k_trace_pt) renders its batches on one pipeline: that traversal is bound
-    // by the latency of its node fetches at 7 waves per SIMD, and a shading launch beside it takes waves
-    // and memory bandwidth from it (C5: 168.4 / 167.9 vs 163.4 / 163.7 Msamples/s); the
-    // LDS-resident scenes keep two (C2 / C3 / C4 gain 2-12 %)
-    if (!s->lds_scene_bytes) s->pipes = 1;
     if (const char* t = std::getenv("PT_HERO_WAVES")) s->hero_waves = std::atoi(t);
     const char* v = std::getenv("PT_SHADE_VARIANT");
     if (v) {
@@ -1903,6 +1898,12 @@ static std::unique_ptr<pt_scene> create_scene_on(int device, const pt_scene_desc
         if (const char* l = std::getenv("PT_LEAF_MIN_W")) s->leaf_min_w = std::max(1, std::atoi(l));
         else if (s->wide_hbm) s->leaf_min_w = s->leaf_min_pt;
     }
+    // A BVH traversed from HBM by the binary walk (k_trace_pt / k_trace_nb: scenes with spheres) renders its
+    // batches on one pipeline: that traversal is bound by the latency of its node fetches at 7 waves per SIMD,
+    // and a shading launch beside it takes waves and memory bandwidth from it (round 5, C5: 168.4 / 167.9 vs
+    // 163.4 / 163.7 Msamples/s). The wide traversal from HBM (k_trace_w<true>) and the
+    // LDS-resident scenes keep two (round 6, C5 @16 spp: 236.7 / 236.2 vs 226.3 / 227.2; C2 / C3 / C4 2-12 %)
+    if (!s->lds_scene_bytes && !s->wide_hbm) s->pipes = 1;
     if (std::getenv("PT_TRACE_DEBUG"))
         std::fprintf(stderr, "[pt] BVH stack rows %d (spill %d), LDS scene %zu B, wide %zu B (%d nodes, %d rows), "
                      "trace kernel %s\n", s->stack_rows, s->trace_spill, s->lds_scene_bytes, s->wide_lds_bytes,

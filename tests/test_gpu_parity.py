@@ -837,16 +837,18 @@ def test_batch_equal_two_pipelines_bit_exact(tmp_path, monkeypatch, equal):
 
 
 def test_default_pipelines_follow_bvh_residency(tmp_path, monkeypatch):
-    """Two pipelines by default for a BVH in LDS, one for a BVH traversed from
-    HBM (PT_TRACE_LDS=0 forces it; C5's case), and both render the oracle's
-    film bit for bit."""
+    """Two pipelines by default for a BVH in LDS and for the wide traversal from
+    HBM (PT_TRACE_LDS=0 forces it; C5's case), one for the binary traversal
+    from HBM (PT_TRACE_WIDE=0 as well: scenes with spheres), and all render the
+    oracle's film bit for bit."""
     from conftest import scene_variant
     monkeypatch.delenv("PT_PIPES", raising=False)
     path = scene_variant(tmp_path, name="portal_cornell.pbrt", res=(64, 48), spp=4)
     hs = ptgpu.HostScene(path)
     ref, rst = pyoracle.render_accum(hs.desc, nthreads=8)
-    for lds, pipes in (("1", 2), ("0", 1)):
+    for lds, wide, pipes in (("1", "1", 2), ("0", "1", 2), ("0", "0", 1)):
         monkeypatch.setenv("PT_TRACE_LDS", lds)
+        monkeypatch.setenv("PT_TRACE_WIDE", wide)
         sc = ptgpu.Scene(hs, batch_slots=16 * 16 * 4 * 3)
         assert sc.query("pipelines") == pipes
         got, gst = sc.render_accum(0, 1)
